@@ -1,0 +1,216 @@
+"""Generates the committed golden fixtures in tests/golden/ (run in the dev container,
+where /root/reference exists; the GPU box only reads the .npz files).
+
+Sources, in order of authority:
+  1. the reference's own known-answer tests, copied as DATA (inputs + expected outputs):
+     tests/libs/test_fft.{infile,outfile.ground} (FFT64 block),
+     code/WiFi/receiver/tests/testViterbi{,Sig11a}.{infile,outfile.ground},
+     code/WiFi/tests/test_encdec_{6,12,18,24,36}mbps.{infile,outfile.ground};
+  2. tables parsed from the reference .blk sources (demap LUTs const.blk:74-150,
+     deinterleaver tables Deinterleave*.blk) = expected outputs of those blocks on
+     identity/index inputs;
+  3. outputs of the reference bricks compiled here from /root/reference/csrc
+     (oracle/_ref/libzref.so via oracle/Makefile.ref): FFT64, Viterbi (all rates), SIGNAL.
+     The .blk glue around them (demap, deinterleave, descramble, CRC) has no C form in the
+     reference (wplc is unavailable), so chain fixtures use the reference FFT + Viterbi
+     bricks with the oracle's glue, which is itself pinned by the encdec KATs above.
+
+Usage: python tests/golden/make_golden.py
+"""
+import ctypes as C
+import os
+import re
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+from oracle import oracle as O  # noqa: E402
+from tests.golden import synth  # noqa: E402
+
+REF = "/root/reference"
+W = REF + "/code/WiFi"
+
+
+def rd(p):
+    txt = open(p).read().replace("\n", ",")
+    return np.array([int(v) for v in txt.split(",") if v.strip() != ""], np.int64)
+
+
+def ptr(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def ref_fft64(R, x):
+    out = np.zeros_like(x)
+    for i in range(x.shape[0]):
+        xi = np.ascontiguousarray(x[i])
+        oi = np.zeros_like(xi)
+        R.zref_sora_fft(ptr(oi), 64, ptr(xi))
+        out[i] = oi
+    return out
+
+
+def ref_viterbi(R, soft, frame_len, code_rate, chunk=48):
+    R.zref_viterbi_init(frame_len, code_rate, 256)
+    buf = np.zeros(12000, np.uint8)
+    outs = []
+    for i in range(0, soft.size, chunk):
+        s = np.ascontiguousarray(soft[i:i + chunk], np.int8)
+        bits = R.zref_viterbi_decode(ptr(s), s.size, ptr(buf), 96000)
+        outs.append(buf[: bits // 8].copy())
+    return np.concatenate(outs) if outs else np.zeros(0, np.uint8)
+
+
+def ref_sig(R, soft48):
+    s = np.ascontiguousarray(soft48, np.int8)
+    o = np.zeros(4, np.uint8)
+    R.zref_viterbi_sig(ptr(s), ptr(o))
+    b = np.unpackbits(o, bitorder="little")[:24].copy()
+    b[18:] = 0
+    return np.packbits(b, bitorder="little")
+
+
+def kats():
+    d = {}
+    inp = rd(REF + "/tests/libs/test_fft.infile")
+    gnd = rd(REF + "/tests/libs/test_fft.outfile.ground")
+    off = sum([12, 16, 24, 32, 36, 48, 60])          # FFT64 is the 8th block of test_fft.wpl
+    d["fft64_kat_in"] = inp[2 * off:2 * off + 128].reshape(64, 2).astype(np.int16)
+    d["fft64_kat_out"] = gnd[2 * off:2 * off + 128].reshape(64, 2).astype(np.int16)
+    d["vit_kat_soft"] = rd(W + "/receiver/tests/testViterbi.infile").astype(np.int8)
+    d["vit_kat_bits"] = rd(W + "/receiver/tests/testViterbi.outfile.ground").astype(np.uint8)
+    d["sig_kat_soft"] = rd(W + "/receiver/tests/testViterbiSig11a.infile")[:48].astype(np.int8)
+    d["sig_kat_bits"] = rd(W + "/receiver/tests/testViterbiSig11a.outfile.ground").astype(np.uint8)
+    for r in (6, 12, 18, 24, 36):
+        base = W + f"/tests/test_encdec_{r}mbps"
+        d[f"encdec_{r}_in"] = rd(base + ".infile").astype(np.int8)
+        d[f"encdec_{r}_out"] = rd(base + ".outfile.ground").astype(np.int8)
+    return d
+
+
+def tables():
+    src = open(W + "/const.blk").read()
+    d = {}
+    for name in ("m_bpsk_lut", "m_qam16_lut2", "m_qam64_lut2", "m_qam64_lut3"):
+        m = re.search(r"let\s+" + name + r"\s*=\s*\{([^}]*)\}", src)
+        d[name] = np.array([int(v) for v in m.group(1).replace("\n", " ").split(",")], np.uint8)
+    for mod, tag in enumerate(("BPSK", "QPSK", "QAM16", "QAM64")):
+        t = open(W + f"/receiver/decoding/Deinterleave{tag}.blk").read()
+        pairs = re.findall(r"output\[(\d+)\]\s*:=\s*symbol\[(\d+)\]", t)
+        n = len(pairs)
+        perm = np.zeros(n, np.int32)
+        for o, i in pairs:
+            perm[int(o)] = int(i)
+        d[f"deint_{mod}"] = perm
+    return d
+
+
+def fft_vectors(R, n=1024, seed=0xF64):
+    rng = np.random.default_rng(seed)
+    x = np.empty((n, 64, 2), np.int16)
+    x[: n // 4] = rng.integers(-32768, 32768, (n // 4, 64, 2))
+    x[n // 4: n // 2] = rng.choice(np.array([-32768, -32767, 32767, 0, 1, -1], np.int16),
+                                  (n // 4, 64, 2))
+    x[n // 2:] = rng.integers(-2500, 2500, (n - n // 2, 64, 2))
+    return {"fft_in": x, "fft_out": ref_fft64(R, x)}
+
+
+def viterbi_vectors(R):
+    d = {}
+    cases = []
+    for cr in (0, 1, 2):
+        for fl in (1, 3, 100, 333, 1500, 4095):
+            for noise in (0, 3, 7, -1):          # -1: uniformly random soft values
+                cases.append((cr, fl, noise))
+    softs, offs, outs, ooffs = [], [0], [], [0]
+    for idx, (cr, fl, noise) in enumerate(cases):
+        s = synth.viterbi_soft(cr, fl, noise, seed=0x5EED + idx)
+        o = ref_viterbi(R, s, fl, cr)
+        softs.append(s)
+        offs.append(offs[-1] + s.size)
+        outs.append(o)
+        ooffs.append(ooffs[-1] + o.size)
+    d["vit_cases"] = np.array(cases, np.int32)
+    d["vit_soft"] = np.concatenate(softs).astype(np.int8)
+    d["vit_soft_off"] = np.array(offs, np.int64)
+    d["vit_out"] = np.concatenate(outs).astype(np.uint8)
+    d["vit_out_off"] = np.array(ooffs, np.int64)
+    # adversarial: patterns that drive metrics toward u8 wrap
+    adv = np.tile(np.array([0, 7, 7, 0, 0, 0, 7, 7, 7, 7, 0, 0], np.int8), 800)[: 48 * 200]
+    for cr in (0, 1, 2):
+        d[f"vit_adv_out_{cr}"] = ref_viterbi(R, adv, 1000, cr)
+    d["vit_adv_soft"] = adv
+    rng = np.random.default_rng(0x516)
+    sig = rng.integers(0, 8, (256, 48)).astype(np.int8)
+    d["sig_soft"] = sig
+    d["sig_bits"] = np.stack([ref_sig(R, s) for s in sig])
+    return d
+
+
+def chain_vectors(R):
+    """54 Mbps time-domain packets (config 3 shape, few packets) and a mixed-MCS batch."""
+    d = {}
+    for tag, plan in (("c54", synth.plan_54mbps(8, 1500)), ("mix", synth.plan_mixed(16, max_len=700))):
+        sym, off, nsym, meta = synth.packets_time(plan, seed=0xC0DE if tag == "c54" else 0x4D1)
+        pays, crcs = [], []
+        for p in range(len(off)):
+            x = sym[off[p]: off[p] + nsym[p]]
+            f = ref_fft64(R, x)                                   # reference FFT brick
+            sub = np.stack([O.get_data(fi) for fi in f])
+            # reference Viterbi brick for the data decode, oracle glue around it
+            pay, ok = ref_chain_from_freq(R, sub)
+            pays.append(pay)
+            crcs.append(ok)
+        d[f"{tag}_sym"] = sym
+        d[f"{tag}_off"] = off
+        d[f"{tag}_nsym"] = nsym
+        d[f"{tag}_meta"] = meta
+        d[f"{tag}_payload"] = np.concatenate(pays)
+        d[f"{tag}_payload_off"] = np.cumsum([0] + [p.size for p in pays]).astype(np.int64)
+        d[f"{tag}_crc"] = np.array(crcs, np.int32)
+    return d
+
+
+def ref_chain_from_freq(R, sub):
+    lim = O.demap_limit(sub[0])
+    soft = O.deinterleave(0, O.demap(0, lim))
+    hb = ref_sig(R, soft)
+    h = O.parse_header(hb)
+    mod, cod, ln = h["modulation"], h["coding"], h["len"]
+    R.zref_viterbi_init(ln + 2, cod, 256)
+    buf = np.zeros(12000, np.uint8)
+    dec = []
+    total = 0
+    for k in range(1, sub.shape[0]):
+        if total >= (ln + 2) * 8:
+            break
+        s = O.deinterleave(mod, O.demap(mod, O.demap_limit(sub[k])))
+        for c in range(0, s.size, 48):
+            ss = np.ascontiguousarray(s[c:c + 48])
+            bits = R.zref_viterbi_decode(ptr(ss), 48, ptr(buf), 96000)
+            dec.append(buf[: bits // 8].copy())
+            total += bits
+    dec = np.concatenate(dec)
+    pay, ok = O.descramble_crc(dec, ln)
+    return pay, int(ok)
+
+
+def main():
+    O.build()
+    R = O.ref()
+    assert R is not None, "reference bricks not built (needs /root/reference)"
+    np.savez_compressed(os.path.join(HERE, "ref_kats.npz"), **kats())
+    np.savez_compressed(os.path.join(HERE, "ref_tables.npz"), **tables())
+    np.savez_compressed(os.path.join(HERE, "ref_fft64.npz"), **fft_vectors(R))
+    np.savez_compressed(os.path.join(HERE, "ref_viterbi.npz"), **viterbi_vectors(R))
+    np.savez_compressed(os.path.join(HERE, "ref_chain.npz"), **chain_vectors(R))
+    for f in sorted(os.listdir(HERE)):
+        if f.endswith(".npz"):
+            print(f, os.path.getsize(os.path.join(HERE, f)))
+
+
+if __name__ == "__main__":
+    main()
