@@ -1,0 +1,139 @@
+/*
+ * ziria_rx.h — C-ABI of the MI355X (gfx950) 802.11a RX decode engine, libziria_rx.so.
+ *
+ * Part 1 re-exports the reference's own external bricks with identical C signatures and
+ * per-call semantics, so Ziria-generated C (wplc output, which calls `__ext_<name>` with
+ * every array argument expanded to (pointer, length), src/Codegen/CgFun.hs:287-316 and
+ * src/Codegen/CgCall.hs:72-130) links against this library unchanged.  Each call runs
+ * on the GPU (batch of one); there is no CPU compute path in this library.
+ *
+ * Part 2 adds batched counterparts over host arrays.  They use only arrays and scalars, so
+ * they can be declared in a .blk file as `fun external` (INTEGRATION.md shows the
+ * declarations).
+ *
+ * Part 3 is the throughput API over device-resident buffers (HBM), asynchronous on a
+ * caller-provided HIP stream; this is what bench.py and the Python engine drive.
+ *
+ * All buffers are caller-owned.  Status-returning functions return ZRX_OK (0) or a
+ * negative ZRX_E* code; the reference's own externals keep their reference return values.
+ */
+#ifndef ZIRIA_RX_H
+#define ZIRIA_RX_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* csrc/numerics.h:113-116 */
+struct complex16 { int16_t re; int16_t im; };
+
+/* ================================================================ Part 1: reference bricks */
+
+/* Replaces __ext_sora_fft (reference csrc/sora_ext_lib.cpp:2672-2812, declared
+ * lib/externals.blk:201-202).  Size 64 (the 802.11a OFDM symbol) runs on the GPU; any
+ * other size prints the reference's error message and leaves `out` untouched, as the
+ * reference does for a size it does not support (:2808-2810). */
+void __ext_sora_fft(struct complex16* out, int nFFTSize, struct complex16* in, int unused1);
+
+/* Replaces __ext_sora_fft_dynamic (sora_ext_lib.cpp:2816-2820, externals.blk:205-206). */
+void __ext_sora_fft_dynamic(struct complex16* out, int unused2, int16_t nFFTSize,
+                            struct complex16* in, int unused1);
+
+/* Replaces __ext_viterbi_brick_init_fast (csrc/sora_ext_viterbi.cpp:48-63,
+ * externals.blk:215).  Resets the (single, global, non-reentrant) streaming decoder. */
+int __ext_viterbi_brick_init_fast(int32_t frame_len, int16_t code_rate, int16_t depth);
+
+/* Replaces __ext_viterbi_brick_decode_fast (sora_ext_viterbi.cpp:66-153,
+ * externals.blk:216): consumes len1 soft values (whole groups), appends the decoded bytes
+ * to `bit` (LSB-first bits), returns the number of bits appended by this call. */
+int16_t __ext_viterbi_brick_decode_fast(int8_t* intInput, int len1, unsigned char* bit, int len2);
+
+/* Replaces __ext_viterbiSig11a_brick_init_fast (sora_ext_viterbi.cpp:158-173). */
+int __ext_viterbiSig11a_brick_init_fast(int32_t frame_len, int16_t code_rate, int16_t depth);
+
+/* Replaces __ext_viterbiSig11a_brick_decode_fast (sora_ext_viterbi.cpp:176-194,
+ * externals.blk:217): 48 soft values -> 24 PLCP bits; like the reference it then shifts
+ * the 32-bit word at `bit` right by 6 (so `bit` must hold 4 bytes).  Returns 0. */
+int16_t __ext_viterbiSig11a_brick_decode_fast(int8_t* intInput, int len1, unsigned char* bit, int len2);
+
+/* Replaces __ext_v_shift_right_complex16 (sora_ext_lib.cpp:1979-1995, externals.blk:110). */
+int __ext_v_shift_right_complex16(struct complex16* z, int unused3, struct complex16* x, int len,
+                                  int shift);
+
+/* ================================================================ Part 2: batched, host arrays */
+
+/* nsym independent 64-point FFTs: in/out hold 64*nsym complex16 (inlen = outlen = 64*nsym). */
+void __ext_sora_fft64_batch(struct complex16* out, int outlen, struct complex16* in, int inlen);
+
+/* Batched Viterbi.  Packet i decodes soft[pkt_soft_off[i] .. pkt_soft_off[i+1]) exactly as
+ * init(frame_len[i], code_rate[i], 256) followed by decode calls over all its soft values,
+ * writing its bytes at out_bits[pkt_out_off[i] ..] (byte offsets; bytes are LSB-first bit
+ * arrays).  pkt_soft_off has npkts+1 entries; every per-packet soft count must be a multiple
+ * of 48.  Returns the number of packets decoded, or a negative ZRX_E* code. */
+int32_t __ext_viterbi_batch_decode(int8_t* soft, int softlen, int32_t* pkt_soft_off, int n_off,
+                                   int32_t* frame_len, int n_fl, int16_t* code_rate, int n_cr,
+                                   unsigned char* out_bits, int out_len_bits,
+                                   int32_t* pkt_out_off, int n_oo);
+
+/* Batched receiveBits (code/WiFi/receiver/receiver.blk:43-54) behind FFT (OFDM/FFT.blk) and
+ * GetData: packet i = symbols [pkt_sym_off[i], pkt_sym_off[i+1]) of `sym` (64 complex16 per
+ * CP-removed OFDM symbol; the first is the SIGNAL symbol).  Writes the descrambled payload
+ * (len-4 bytes) of packet i at payload[i*4096 ..] and pkt_info[8*i ..] = {modulation,
+ * coding, len, header_err, crc_ok, status, symbols_used, viterbi_bits}.
+ * Returns the number of packets whose CRC passed, or a negative ZRX_E* code. */
+int32_t __ext_wifi_rx_batch(struct complex16* sym, int nsym_total, int32_t* pkt_sym_off, int n_off,
+                            unsigned char* payload, int payload_len_bits,
+                            int32_t* pkt_info, int n_info);
+
+/* ================================================================ Part 3: device API */
+
+#define ZRX_OK 0
+#define ZRX_EINVAL (-1)    /* bad argument (sizes, rates, soft count not a group multiple) */
+#define ZRX_EHIP (-2)      /* HIP runtime error */
+#define ZRX_ENOMEM (-3)    /* workspace too small / allocation failed */
+#define ZRX_ENODEV (-4)    /* no gfx950 device */
+
+/* packet status in pkt_info[5] */
+#define ZRX_PKT_OK 0
+#define ZRX_PKT_HDR_ERR 1      /* PLCP header parity/tail/length error: no payload (as the reference) */
+#define ZRX_PKT_TRUNCATED 2    /* fewer symbols than the header requires */
+
+typedef struct zrx_ctx zrx_ctx;
+
+/* Engine context on `device` issuing on `stream` (hipStream_t, may be NULL = default). */
+int zrx_create(zrx_ctx** ctx, int device, void* stream);
+int zrx_destroy(zrx_ctx* ctx);
+int zrx_set_stream(zrx_ctx* ctx, void* stream);
+/* Pre-allocates the workspace for rx batches of up to npkts packets whose largest
+ * packet has max_nsym symbols (no allocation happens inside the launch functions). */
+int zrx_reserve(zrx_ctx* ctx, int npkts, int max_nsym);
+/* Per-stage HIP-event timing on the context's stream (0 = off). */
+int zrx_enable_timing(zrx_ctx* ctx, int on);
+/* Stage durations (ms) of the last launch: [0] SIGNAL FFT+demap, [1] SIGNAL Viterbi+header,
+ * [2] data FFT+demap+deinterleave, [3] data Viterbi, [4] descramble+CRC.  Synchronizes. */
+int zrx_get_timing(zrx_ctx* ctx, float* ms5);
+
+/* d_in/d_out: 64*nsym complex16 each (may alias). */
+int zrx_fft64_dev(zrx_ctx* ctx, const struct complex16* d_in, struct complex16* d_out, int64_t nsym);
+
+/* d_params: 4 int32 per packet {frame_len, code_rate, soft_len, 0}; d_soft_off, d_out_off:
+ * int64 byte offsets per packet; d_out_bits: int32 per packet (bits written). */
+int zrx_viterbi_dev(zrx_ctx* ctx, const int8_t* d_soft, const int64_t* d_soft_off,
+                    const int32_t* d_params, int npkts, uint8_t* d_out, const int64_t* d_out_off,
+                    int32_t* d_out_bits);
+
+/* Full chain; d_sym_off: int64 symbol index of each packet's SIGNAL symbol; d_nsym: int32
+ * symbols available per packet; max_nsym: bound on d_nsym (grid sizing).  d_payload holds
+ * npkts*4096 bytes, d_info npkts*8 int32 (layout as __ext_wifi_rx_batch). */
+int zrx_rx_dev(zrx_ctx* ctx, const struct complex16* d_sym, const int64_t* d_sym_off,
+               const int32_t* d_nsym, int npkts, int max_nsym, uint8_t* d_payload,
+               int32_t* d_info);
+
+/* Version / build string. */
+const char* zrx_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

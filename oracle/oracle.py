@@ -75,6 +75,13 @@ def fft64(x):
     return out.reshape(x.shape)
 
 
+def v_shift_right_complex16(x, shift):
+    x = np.ascontiguousarray(x, dtype=np.int16).reshape(-1, 2)
+    z = np.zeros_like(x)
+    lib().zo_v_shift_right_complex16(_p(z), _p(x), x.shape[0], int(shift))
+    return z
+
+
 def get_data(f64):
     f64 = np.ascontiguousarray(f64, dtype=np.int16).reshape(64, 2)
     o = np.empty((48, 2), np.int16)

@@ -87,6 +87,20 @@ void zo_fft64(const zo_c16* in, zo_c16* out) {
   for (int i = 0; i < 64; i++) out[i] = x[bitrev6(i)];
 }
 
+/* __ext_v_shift_right_complex16 (csrc/sora_ext_lib.cpp:1979-1995): whole groups of 4
+   complex values use _mm_srai_epi16 (arithmetic, counts > 15 fill with the sign); the
+   remaining values use unum16 >> shift (logical). */
+int zo_v_shift_right_complex16(zo_c16* z, const zo_c16* x, int len, int shift) {
+  const int16_t* P = (const int16_t*)x;
+  int16_t* Q = (int16_t*)z;
+  int nvec = (len / 4) * 8;
+  for (int i = 0; i < 2 * len; i++) {
+    if (i < nvec) Q[i] = (int16_t)((shift < 0 || shift > 15) ? (P[i] < 0 ? -1 : 0) : (P[i] >> shift));
+    else Q[i] = (int16_t)((shift < 0 || shift > 15) ? 0 : ((uint16_t)P[i] >> shift));
+  }
+  return 0;
+}
+
 /* ------------------------------------------------------------------------------------ */
 /* GetData.blk:24-35: bins 38..42, 44..56, 58..63, 1..6, 8..20, 22..26 */
 void zo_get_data(const zo_c16* s, zo_c16* o) {

@@ -26,6 +26,8 @@ void zo_fft64(const zo_c16* in, zo_c16* out);
 /* twiddles twFFTLUT{N}_{k} (csrc/sora_ext_lib_fft_coeffs.hpp:53-78,298-359) regenerated */
 void zo_twiddle(int N, int k, int n, int16_t* re, int16_t* im);
 
+int  zo_v_shift_right_complex16(zo_c16* z, const zo_c16* x, int len, int shift);  /* sora_ext_lib.cpp:1979 */
+
 /* ---- GetData / DemapLimit / Demap* / Deinterleave* (code/WiFi/receiver/...) ---- */
 void zo_get_data(const zo_c16* sym64, zo_c16* out48);            /* OFDM/GetData.blk:24-35 */
 void zo_demap_limit(const zo_c16* in, int n, zo_c16* out);        /* decoding/DemapLimit.blk:22-63 */

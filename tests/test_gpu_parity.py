@@ -1,0 +1,242 @@
+"""GPU parity: the HIP engine (through the C-ABI of libziria_rx.so) against the oracle, the
+reference's own KATs and the reference-brick golden fixtures.  Integer/byte work, so every
+comparison is bit-exact (no tolerance)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+import ziria_amd as Z  # noqa: E402
+from ziria_amd import txgen  # noqa: E402
+from ziria_amd.engine import RxEngine  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def engine():
+    e = RxEngine(0)
+    yield e
+    e.close()
+
+
+def test_library_is_native():
+    assert Z.lib().zrx_version().startswith(b"ziria_rx")
+
+
+# ------------------------------------------------------------------ FFT64
+def test_fft64_kat(golden):
+    k = golden["ref_kats"]
+    out = Z.sora_fft(k["fft64_kat_in"])
+    assert (out == k["fft64_kat_out"]).all()
+
+
+def test_fft64_reference_vectors(golden):
+    g = golden["ref_fft64"]
+    out = Z.sora_fft64_batch(g["fft_in"])
+    assert (out == g["fft_out"]).all()
+
+
+def test_fft64_device_random_vs_oracle(engine, oracle):
+    rng = np.random.default_rng(11)
+    x = rng.integers(-32768, 32768, (3000, 64, 2)).astype(np.int16)
+    x[:500] = rng.choice(np.array([-32768, 32767, -1, 0], np.int16), (500, 64, 2))
+    out = engine.fft64(torch.from_numpy(x).cuda()).cpu().numpy()
+    assert (out == oracle.fft64(x)).all()
+
+
+def test_fft_unsupported_size_leaves_output():
+    x = np.ones((32, 2), np.int16)
+    assert (Z.sora_fft(x) == 0).all()
+    assert (Z.sora_fft_dynamic(64, np.ones((64, 2), np.int16)) ==
+            Z.sora_fft(np.ones((64, 2), np.int16))).all()
+
+
+def test_v_shift_right_complex16(oracle):
+    rng = np.random.default_rng(5)
+    for n in (1, 3, 4, 5, 8, 13):
+        for sh in (0, 1, 7, 15, 16):
+            x = rng.integers(-32768, 32768, (n, 2)).astype(np.int16)
+            assert (Z.v_shift_right_complex16(x, sh) == oracle.v_shift_right_complex16(x, sh)).all()
+
+
+# ------------------------------------------------------------------ Viterbi
+def test_viterbi_kat(golden):
+    k = golden["ref_kats"]
+    Z.viterbi_brick_init_fast(100, 0, 256)
+    outs = []
+    s = k["vit_kat_soft"]
+    for i in range(0, s.size, 48):
+        nb, b = Z.viterbi_brick_decode_fast(s[i:i + 48])
+        outs.append(b)
+    bits = np.unpackbits(np.concatenate(outs), bitorder="little")
+    assert (bits == k["vit_kat_bits"]).all()
+
+
+def _vit_cases(golden):
+    g = golden["ref_viterbi"]
+    return g, g["vit_cases"], g["vit_soft_off"], g["vit_out_off"]
+
+
+def test_viterbi_batch_reference_frames(golden):
+    g, cases, so, oo = _vit_cases(golden)
+    fl = cases[:, 1].astype(np.int32)
+    cr = cases[:, 0].astype(np.int16)
+    out, off = Z.viterbi_batch_decode(g["vit_soft"], so.astype(np.int32), fl, cr)
+    for i in range(len(cases)):
+        exp = g["vit_out"][oo[i]:oo[i + 1]]
+        got = out[off[i]:off[i] + exp.size]
+        assert (got == exp).all(), f"case {tuple(cases[i])}"
+
+
+def test_viterbi_adversarial_wrap(golden):
+    g = golden["ref_viterbi"]
+    s = g["vit_adv_soft"]
+    for cr in (0, 1, 2):
+        out, _ = Z.viterbi_batch_decode(s, np.array([0, s.size], np.int32), np.array([1000], np.int32),
+                                        np.array([cr], np.int16))
+        exp = g[f"vit_adv_out_{cr}"]
+        assert (out[:exp.size] == exp).all()
+
+
+def test_viterbi_per_call_stream(golden):
+    g, cases, so, oo = _vit_cases(golden)
+    for i, (cr, fl, noise) in enumerate(cases):
+        if fl not in (1, 3, 333) or noise not in (3, -1):
+            continue
+        Z.viterbi_brick_init_fast(int(fl), int(cr), 256)
+        s = g["vit_soft"][so[i]:so[i + 1]]
+        outs = []
+        for k in range(0, s.size, 48):
+            nb, b = Z.viterbi_brick_decode_fast(s[k:k + 48])
+            assert nb == 8 * b.size
+            outs.append(b)
+        got = np.concatenate(outs)
+        assert (got == g["vit_out"][oo[i]:oo[i + 1]]).all(), f"case {(cr, fl, noise)}"
+
+
+def test_viterbi_batch_random_vs_oracle(oracle):
+    rng = np.random.default_rng(77)
+    softs, offs, fls, crs = [], [0], [], []
+    for i in range(67):                          # not a multiple of 4 packets per block
+        cr = int(rng.integers(0, 3))
+        fl = int(rng.integers(1, 700))
+        from tests.golden import synth
+        s = synth.viterbi_soft(cr, fl, int(rng.integers(-1, 5)), seed=1000 + i)
+        if i % 5 == 0:
+            s = s[: max(48, (s.size // 2) // 48 * 48)]      # truncated: decoder stops mid-frame
+        softs.append(s); offs.append(offs[-1] + s.size); fls.append(fl); crs.append(cr)
+    soft = np.concatenate(softs)
+    out, off = Z.viterbi_batch_decode(soft, np.array(offs, np.int32), np.array(fls, np.int32),
+                                      np.array(crs, np.int16))
+    for i in range(len(fls)):
+        exp = oracle.viterbi_decode(soft[offs[i]:offs[i + 1]], fls[i], crs[i])
+        assert (out[off[i]:off[i] + exp.size] == exp).all(), i
+
+
+def test_viterbi_empty_batch():
+    out, off = Z.viterbi_batch_decode(np.zeros(0, np.int8), np.array([0], np.int32),
+                                      np.zeros(0, np.int32), np.zeros(0, np.int16))
+    assert off.size == 0
+
+
+# ------------------------------------------------------------------ SIGNAL
+def test_signal_kat(golden):
+    k = golden["ref_kats"]
+    w = Z.viterbiSig11a_brick_decode_fast(k["sig_kat_soft"])
+    bits = np.unpackbits(w, bitorder="little")[:24].copy()
+    bits[18:] = 0
+    assert (bits == k["sig_kat_bits"]).all()
+
+
+def test_signal_reference_vectors(golden):
+    g = golden["ref_viterbi"]
+    for s, exp in zip(g["sig_soft"], g["sig_bits"]):
+        w = Z.viterbiSig11a_brick_decode_fast(s)
+        b = np.unpackbits(w, bitorder="little")[:24].copy()
+        b[18:] = 0
+        assert (np.packbits(b, bitorder="little") == exp).all()
+
+
+# ------------------------------------------------------------------ full chain
+def _check_chain(pay, info, exp_pay, exp_off, exp_crc, meta):
+    for i in range(len(exp_crc)):
+        mod, cod, ln = meta[i]
+        assert info["modulation"][i] == mod and info["coding"][i] == cod and info["len"][i] == ln
+        assert info["crc_ok"][i] == exp_crc[i], i
+        e = exp_pay[exp_off[i]:exp_off[i + 1]]
+        assert (pay[i, :e.size] == e).all(), i
+
+
+@pytest.mark.parametrize("tag", ["c54", "mix"])
+def test_chain_reference_packets(golden, tag):
+    g = golden["ref_chain"]
+    sym, off, nsym = g[f"{tag}_sym"], g[f"{tag}_off"], g[f"{tag}_nsym"]
+    csr = np.concatenate([off, [off[-1] + nsym[-1]]]).astype(np.int32)
+    pay, info, nok = Z.wifi_rx_batch(sym, csr)
+    _check_chain(pay, info, g[f"{tag}_payload"], g[f"{tag}_payload_off"], g[f"{tag}_crc"], g[f"{tag}_meta"])
+    assert nok == int(g[f"{tag}_crc"].sum())
+
+
+def test_chain_device_engine_54mbps(engine, oracle):
+    b = txgen.make_batch(257, seed=99, device="cuda")
+    engine.reserve(257, b["max_nsym"])
+    pay, info = engine.rx(b["sym"], b["sym_off"], b["nsym"], b["max_nsym"])
+    pay, info = pay.cpu().numpy(), info.cpu().numpy()
+    assert (info[:, 4] == 1).all() and (info[:, 5] == 0).all()
+    assert (pay[:, :1500] == b["payload"]).all()
+    opay, ores = oracle.rx_batch_time(b["sym"].cpu().numpy(), b["sym_off"].cpu().numpy(),
+                                      b["nsym"].cpu().numpy(), nthreads=8)
+    assert (pay[:, :1500] == opay[:, :1500]).all()
+    assert all(r["crc_ok"] == 1 for r in ores)
+
+
+def test_chain_mixed_mcs_vs_oracle(engine, oracle):
+    m = txgen.make_mixed(96, max_len=2200, sigma=3.0, seed=5, device="cuda")
+    n = m["sym_off"].numel()
+    engine.reserve(n, m["max_nsym"])
+    pay, info = engine.rx(m["sym"], m["sym_off"], m["nsym"], m["max_nsym"])
+    pay, info = pay.cpu().numpy(), info.cpu().numpy()
+    opay, ores = oracle.rx_batch_time(m["sym"].cpu().numpy(), m["sym_off"].cpu().numpy(),
+                                      m["nsym"].cpu().numpy(), nthreads=8)
+    for i in range(n):
+        r = ores[i]
+        assert (info[i, 0], info[i, 1], info[i, 2], info[i, 3]) == (r["modulation"], r["coding"], r["len"], r["err"])
+        if r["err"]:
+            assert info[i, 5] == 1 and info[i, 4] == 0
+            continue
+        assert info[i, 4] == r["crc_ok"]
+        L = r["len"] - 4
+        assert (pay[i, :L] == opay[i, :L]).all(), i
+    ok = info[:, 3] == 0
+    assert ok.sum() > 40 and (info[ok, 4] == 1).all()
+
+
+def test_chain_truncated_and_bad_header(engine, oracle):
+    b = txgen.make_batch(8, seed=4, device="cuda")
+    sym = b["sym"].clone()
+    nsym = b["nsym"].clone()
+    nsym[1] = 10                                # fewer symbols than the header needs
+    S = b["max_nsym"]
+    sym[2 * S] = 0                              # zeroed SIGNAL symbol -> header garbage
+    engine.reserve(8, S)
+    pay, info = engine.rx(sym, b["sym_off"], nsym, S)
+    info = info.cpu().numpy()
+    assert info[1, 5] == 2 and info[1, 4] == 0
+    _, r2 = oracle.rx_packet_time(sym[2 * S:3 * S].cpu().numpy())
+    assert (info[2, 0], info[2, 1], info[2, 2], info[2, 3]) == (r2["modulation"], r2["coding"], r2["len"], r2["err"])
+    for i in (0, 3, 4, 5, 6, 7):
+        assert info[i, 4] == 1
+
+
+def test_chain_large_batch_properties(engine):
+    """Full-size property check at config-3 shape: every CRC passes and every payload
+    equals what was transmitted."""
+    b = txgen.make_batch(4096, seed=1234, device="cuda")
+    engine.reserve(4096, b["max_nsym"])
+    pay, info = engine.rx(b["sym"], b["sym_off"], b["nsym"], b["max_nsym"])
+    info = info.cpu().numpy()
+    assert (info[:, 4] == 1).all()
+    assert (pay[:, :1500].cpu().numpy() == b["payload"]).all()

@@ -1,0 +1,40 @@
+"""Builds libziria_rx.so (all HIP kernels + the C-ABI) in-tree for gfx950 with hipcc.
+
+The library is the product: ziria_amd's Python layer only loads it.  Output:
+ziria_amd/_lib/libziria_rx.so (git-ignored, travels to the GPU box with the snapshot).
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "_lib")
+LIB = os.path.join(LIBDIR, "libziria_rx.so")
+SOURCES = ["zrx_api.hip", "zrx_kernels.hip", "zrx_device.hpp", "zrx_tables.h", "gen_tables.py"]
+
+
+def _stale():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(HERE, "..", "include", "ziria_rx.h")]
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build(force=False, verbose=False):
+    if not force and not _stale():
+        return LIB
+    os.makedirs(LIBDIR, exist_ok=True)
+    subprocess.check_call([sys.executable, os.path.join(CSRC, "gen_tables.py")])
+    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wall", "-o", LIB + ".tmp", os.path.join(CSRC, "zrx_api.hip")]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd, cwd=CSRC)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,438 @@
+// Host side of libziria_rx.so: the C-ABI of include/ziria_rx.h.
+//
+// Everything that computes runs in the HIP kernels of zrx_kernels.hip on a gfx950 device;
+// this file only validates arguments, stages buffers and launches.  Without a usable GPU
+// every entry point fails loudly (message on stderr + error code); there is no CPU path.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/ziria_rx.h"
+#include "zrx_kernels.hip"
+
+using namespace zrx;
+
+#define ZRX_CHECK(call)                                                                   \
+  do {                                                                                    \
+    hipError_t e_ = (call);                                                               \
+    if (e_ != hipSuccess) {                                                               \
+      std::fprintf(stderr, "ziria_rx: HIP error %s at %s:%d\n", hipGetErrorString(e_),   \
+                   __FILE__, __LINE__);                                                   \
+      return ZRX_EHIP;                                                                    \
+    }                                                                                     \
+  } while (0)
+
+struct zrx_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool timing = false;
+  hipEvent_t ev[6] = {};
+  // rx-chain workspace (zrx_reserve)
+  int cap_pkts = 0, cap_nsym = 0;
+  int64_t soft_stride = 0;
+  uint32_t* sig_soft = nullptr;   // 48 B per packet
+  int32_t* vparams = nullptr;     // 4 int32 per packet
+  uint8_t* soft = nullptr;        // soft_stride B per packet
+  int64_t* soft_off = nullptr;    // p * soft_stride
+  uint8_t* dec = nullptr;         // kDecStride B per packet
+  int64_t* dec_off = nullptr;     // p * kDecStride
+  int32_t* dec_bits = nullptr;
+  // per-call externals
+  VitStream* vstream = nullptr;
+  void* small = nullptr;          // staging for single calls
+  size_t small_cap = 0;
+};
+
+static int check_device(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= device) {
+    std::fprintf(stderr, "ziria_rx: no HIP device %d available (this engine has no CPU path)\n", device);
+    return ZRX_ENODEV;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return ZRX_ENODEV;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    std::fprintf(stderr, "ziria_rx: device %d is %s, this build targets gfx950\n", device, prop.gcnArchName);
+    return ZRX_ENODEV;
+  }
+  return ZRX_OK;
+}
+
+static void free_ws(zrx_ctx* c) {
+  for (void* p : {(void*)c->sig_soft, (void*)c->vparams, (void*)c->soft, (void*)c->soft_off, (void*)c->dec,
+                  (void*)c->dec_off, (void*)c->dec_bits})
+    (void)hipFree(p);
+  c->sig_soft = nullptr; c->vparams = nullptr; c->soft = nullptr; c->soft_off = nullptr;
+  c->dec = nullptr; c->dec_off = nullptr; c->dec_bits = nullptr;
+  c->cap_pkts = c->cap_nsym = 0;
+}
+
+__global__ void k_fill_offsets(int64_t* off, int n, int64_t stride) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) off[i] = (int64_t)i * stride;
+}
+
+static inline int blocks(int64_t n, int per) { return (int)((n + per - 1) / per); }
+
+extern "C" {
+
+const char* zrx_version(void) { return "ziria_rx 0.1 (gfx950)"; }
+
+int zrx_create(zrx_ctx** out, int device, void* stream) {
+  if (!out) return ZRX_EINVAL;
+  *out = nullptr;
+  int rc = check_device(device);
+  if (rc) return rc;
+  ZRX_CHECK(hipSetDevice(device));
+  zrx_ctx* c = new zrx_ctx();
+  c->device = device;
+  c->stream = (hipStream_t)stream;
+  for (auto& e : c->ev) ZRX_CHECK(hipEventCreate(&e));
+  *out = c;
+  return ZRX_OK;
+}
+
+int zrx_destroy(zrx_ctx* c) {
+  if (!c) return ZRX_OK;
+  (void)hipSetDevice(c->device);
+  free_ws(c);
+  (void)hipFree(c->vstream);
+  (void)hipFree(c->small);
+  for (auto& e : c->ev) (void)hipEventDestroy(e);
+  delete c;
+  return ZRX_OK;
+}
+
+int zrx_set_stream(zrx_ctx* c, void* stream) {
+  if (!c) return ZRX_EINVAL;
+  c->stream = (hipStream_t)stream;
+  return ZRX_OK;
+}
+
+int zrx_enable_timing(zrx_ctx* c, int on) {
+  if (!c) return ZRX_EINVAL;
+  c->timing = on != 0;
+  return ZRX_OK;
+}
+
+int zrx_get_timing(zrx_ctx* c, float* ms5) {
+  if (!c || !ms5) return ZRX_EINVAL;
+  ZRX_CHECK(hipEventSynchronize(c->ev[5]));
+  for (int i = 0; i < 5; i++) ZRX_CHECK(hipEventElapsedTime(&ms5[i], c->ev[i], c->ev[i + 1]));
+  return ZRX_OK;
+}
+
+int zrx_reserve(zrx_ctx* c, int npkts, int max_nsym) {
+  if (!c || npkts < 0 || max_nsym < 1) return ZRX_EINVAL;
+  if (npkts <= c->cap_pkts && max_nsym <= c->cap_nsym) return ZRX_OK;
+  ZRX_CHECK(hipSetDevice(c->device));
+  const int np = std::max(npkts, c->cap_pkts), ns = std::max(max_nsym, c->cap_nsym);
+  free_ws(c);
+  const int64_t stride = ((int64_t)std::max(ns - 1, 1) * 288 + 255) / 256 * 256;
+  ZRX_CHECK(hipMalloc(&c->sig_soft, (size_t)np * 48 + 16));
+  ZRX_CHECK(hipMalloc(&c->vparams, (size_t)np * 16 + 16));
+  ZRX_CHECK(hipMalloc(&c->soft, (size_t)np * stride + 256));
+  ZRX_CHECK(hipMalloc(&c->soft_off, (size_t)np * 8 + 8));
+  ZRX_CHECK(hipMalloc(&c->dec, (size_t)np * kDecStride + 256));
+  ZRX_CHECK(hipMalloc(&c->dec_off, (size_t)np * 8 + 8));
+  ZRX_CHECK(hipMalloc(&c->dec_bits, (size_t)np * 4 + 4));
+  if (np > 0) {
+    k_fill_offsets<<<blocks(np, 256), 256, 0, c->stream>>>(c->soft_off, np, stride);
+    k_fill_offsets<<<blocks(np, 256), 256, 0, c->stream>>>(c->dec_off, np, kDecStride);
+    ZRX_CHECK(hipGetLastError());
+  }
+  ZRX_CHECK(hipStreamSynchronize(c->stream));
+  c->cap_pkts = np; c->cap_nsym = ns; c->soft_stride = stride;
+  return ZRX_OK;
+}
+
+int zrx_fft64_dev(zrx_ctx* c, const struct complex16* d_in, struct complex16* d_out, int64_t nsym) {
+  if (!c || nsym < 0 || (nsym > 0 && (!d_in || !d_out))) return ZRX_EINVAL;
+  if (nsym == 0) return ZRX_OK;
+  k_fft64<<<blocks(nsym, 256), 256, 0, c->stream>>>((const uint4*)d_in, (uint4*)d_out, nsym);
+  ZRX_CHECK(hipGetLastError());
+  return ZRX_OK;
+}
+
+int zrx_viterbi_dev(zrx_ctx* c, const int8_t* d_soft, const int64_t* d_soft_off, const int32_t* d_params,
+                    int npkts, uint8_t* d_out, const int64_t* d_out_off, int32_t* d_out_bits) {
+  if (!c || npkts < 0) return ZRX_EINVAL;
+  if (npkts == 0) return ZRX_OK;
+  k_viterbi<<<blocks(npkts, 4), 256, 0, c->stream>>>((const uint8_t*)d_soft, d_soft_off, d_params, npkts, d_out,
+                                                       d_out_off, d_out_bits, 256);
+  ZRX_CHECK(hipGetLastError());
+  return ZRX_OK;
+}
+
+int zrx_rx_dev(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_sym_off, const int32_t* d_nsym,
+               int npkts, int max_nsym, uint8_t* d_payload, int32_t* d_info) {
+  if (!c || npkts < 0 || max_nsym < 1) return ZRX_EINVAL;
+  if (npkts > c->cap_pkts || max_nsym > c->cap_nsym) {
+    std::fprintf(stderr, "ziria_rx: workspace holds %d packets x %d symbols, call zrx_reserve(%d, %d)\n",
+                 c->cap_pkts, c->cap_nsym, npkts, max_nsym);
+    return ZRX_ENOMEM;
+  }
+  if (npkts == 0) return ZRX_OK;
+  hipStream_t s = c->stream;
+  if (c->timing) ZRX_CHECK(hipEventRecord(c->ev[0], s));
+  k_signal_fft<<<blocks(npkts, 256), 256, 0, s>>>((const uint4*)d_sym, d_sym_off, d_nsym, npkts, (uint4*)c->sig_soft);
+  if (c->timing) ZRX_CHECK(hipEventRecord(c->ev[1], s));
+  k_signal_vit<<<blocks(npkts, 4), 256, 0, s>>>(c->sig_soft, d_nsym, npkts, c->vparams, d_info);
+  if (c->timing) ZRX_CHECK(hipEventRecord(c->ev[2], s));
+  k_data_fft<<<blocks(npkts, 4), 256, 0, s>>>((const uint4*)d_sym, d_sym_off, c->vparams, npkts, (uint4*)c->soft,
+                                              c->soft_off);
+  if (c->timing) ZRX_CHECK(hipEventRecord(c->ev[3], s));
+  k_viterbi<<<blocks(npkts, 4), 256, 0, s>>>(c->soft, c->soft_off, c->vparams, npkts, c->dec, c->dec_off,
+                                             c->dec_bits, 256);
+  if (c->timing) ZRX_CHECK(hipEventRecord(c->ev[4], s));
+  k_descramble_crc<<<blocks(npkts, 4), 256, 0, s>>>(c->dec, c->dec_bits, d_info, d_payload, npkts);
+  if (c->timing) ZRX_CHECK(hipEventRecord(c->ev[5], s));
+  ZRX_CHECK(hipGetLastError());
+  return ZRX_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ default context (per-call API)
+static std::mutex g_mu;
+static zrx_ctx* g_ctx = nullptr;
+
+static zrx_ctx* default_ctx() {
+  if (g_ctx) return g_ctx;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  if (zrx_create(&g_ctx, dev, nullptr) != ZRX_OK) {
+    std::fprintf(stderr, "ziria_rx: cannot create a GPU context; the externals have no CPU path\n");
+    std::abort();   // the reference would be unusable too; fail loudly rather than compute wrongly
+  }
+  return g_ctx;
+}
+
+static void* staging(zrx_ctx* c, size_t bytes) {
+  if (bytes > c->small_cap) {
+    (void)hipFree(c->small);
+    c->small = nullptr;
+    size_t cap = std::max<size_t>(bytes, 1 << 20);
+    if (hipMalloc(&c->small, cap) != hipSuccess) { c->small_cap = 0; return nullptr; }
+    c->small_cap = cap;
+  }
+  return c->small;
+}
+
+#define ZRX_DIE(msg)                                                     \
+  do {                                                                   \
+    std::fprintf(stderr, "ziria_rx: %s (%s:%d)\n", msg, __FILE__, __LINE__); \
+    std::abort();                                                        \
+  } while (0)
+#define ZRX_OR_DIE(call) \
+  do { if ((call) != hipSuccess) ZRX_DIE(#call); } while (0)
+
+extern "C" {
+
+void __ext_sora_fft(struct complex16* out, int nFFTSize, struct complex16* in, int unused1) {
+  (void)unused1;
+  if (nFFTSize != 64) {
+    std::printf("__ext_sora_fft error: fft size %d not supported!\n", nFFTSize);   // :2808-2810
+    return;
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  zrx_ctx* c = default_ctx();
+  uint8_t* d = (uint8_t*)staging(c, 512);
+  if (!d) ZRX_DIE("staging allocation failed");
+  ZRX_OR_DIE(hipMemcpyAsync(d, in, 256, hipMemcpyHostToDevice, c->stream));
+  k_fft64<<<1, 64, 0, c->stream>>>((const uint4*)d, (uint4*)(d + 256), 1);
+  ZRX_OR_DIE(hipGetLastError());
+  ZRX_OR_DIE(hipMemcpyAsync(out, d + 256, 256, hipMemcpyDeviceToHost, c->stream));
+  ZRX_OR_DIE(hipStreamSynchronize(c->stream));
+}
+
+void __ext_sora_fft_dynamic(struct complex16* out, int unused2, int16_t nFFTSize, struct complex16* in, int unused1) {
+  (void)unused2;
+  __ext_sora_fft(out, nFFTSize, in, unused1);
+}
+
+static int vit_init_impl(int32_t frame_len, int16_t code_rate, int16_t depth) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  zrx_ctx* c = default_ctx();
+  if (!c->vstream) ZRX_OR_DIE(hipMalloc(&c->vstream, sizeof(VitStream)));
+  k_vit_init<<<1, 64, 0, c->stream>>>(c->vstream, frame_len, code_rate, depth);
+  ZRX_OR_DIE(hipGetLastError());
+  ZRX_OR_DIE(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int __ext_viterbi_brick_init_fast(int32_t frame_len, int16_t code_rate, int16_t depth) {
+  return vit_init_impl(frame_len, code_rate, depth);
+}
+int __ext_viterbiSig11a_brick_init_fast(int32_t frame_len, int16_t code_rate, int16_t depth) {
+  return vit_init_impl(frame_len, code_rate, depth);    // the reference resets the same decoder
+}
+
+int16_t __ext_viterbi_brick_decode_fast(int8_t* intInput, int len1, unsigned char* bit, int len2) {
+  (void)len2;
+  if (len1 <= 0) return 0;
+  std::lock_guard<std::mutex> lk(g_mu);
+  zrx_ctx* c = default_ctx();
+  if (!c->vstream) ZRX_DIE("__ext_viterbi_brick_decode_fast before __ext_viterbi_brick_init_fast");
+  const size_t out_cap = (size_t)len1 + 512;
+  uint8_t* d = (uint8_t*)staging(c, (size_t)len1 + out_cap + 64);
+  if (!d) ZRX_DIE("staging allocation failed");
+  uint8_t* d_out = d + ((len1 + 15) / 16) * 16;
+  int32_t* d_bits = (int32_t*)(d_out + out_cap);
+  ZRX_OR_DIE(hipMemcpyAsync(d, intInput, (size_t)len1, hipMemcpyHostToDevice, c->stream));
+  k_viterbi_stream<<<1, 64, 0, c->stream>>>(c->vstream, d, len1, d_out, d_bits);
+  ZRX_OR_DIE(hipGetLastError());
+  int32_t bits = 0;
+  ZRX_OR_DIE(hipMemcpyAsync(&bits, d_bits, 4, hipMemcpyDeviceToHost, c->stream));
+  ZRX_OR_DIE(hipStreamSynchronize(c->stream));
+  if (bits > 0) {
+    ZRX_OR_DIE(hipMemcpyAsync(bit, d_out, (size_t)bits / 8, hipMemcpyDeviceToHost, c->stream));
+    ZRX_OR_DIE(hipStreamSynchronize(c->stream));
+  }
+  return (int16_t)bits;
+}
+
+int16_t __ext_viterbiSig11a_brick_decode_fast(int8_t* intInput, int len1, unsigned char* bit, int len2) {
+  (void)len1; (void)len2;
+  std::lock_guard<std::mutex> lk(g_mu);
+  zrx_ctx* c = default_ctx();
+  uint8_t* d = (uint8_t*)staging(c, 128);
+  if (!d) ZRX_DIE("staging allocation failed");
+  ZRX_OR_DIE(hipMemcpyAsync(d, intInput, 48, hipMemcpyHostToDevice, c->stream));
+  k_sig_bytes<<<1, 64, 0, c->stream>>>((const uint32_t*)d, 1, d + 64);
+  ZRX_OR_DIE(hipGetLastError());
+  ZRX_OR_DIE(hipMemcpyAsync(bit, d + 64, 3, hipMemcpyDeviceToHost, c->stream));
+  ZRX_OR_DIE(hipStreamSynchronize(c->stream));
+  uint32_t w;
+  std::memcpy(&w, bit, 4);
+  w >>= 6;                                            // *((unum32 *)bit) >>= 6  (:191)
+  std::memcpy(bit, &w, 4);
+  return 0;
+}
+
+int __ext_v_shift_right_complex16(struct complex16* z, int unused3, struct complex16* x, int len, int shift) {
+  (void)unused3;
+  if (len <= 0) return 0;
+  std::lock_guard<std::mutex> lk(g_mu);
+  zrx_ctx* c = default_ctx();
+  const size_t bytes = (size_t)len * 4;
+  uint8_t* d = (uint8_t*)staging(c, 2 * bytes + 64);
+  if (!d) ZRX_DIE("staging allocation failed");
+  uint8_t* dz = d + ((bytes + 15) / 16) * 16;
+  ZRX_OR_DIE(hipMemcpyAsync(d, x, bytes, hipMemcpyHostToDevice, c->stream));
+  k_shift_right<<<blocks(2 * (int64_t)len, 256), 256, 0, c->stream>>>((const uint16_t*)d, (uint16_t*)dz, len, shift);
+  ZRX_OR_DIE(hipGetLastError());
+  ZRX_OR_DIE(hipMemcpyAsync(z, dz, bytes, hipMemcpyDeviceToHost, c->stream));
+  ZRX_OR_DIE(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+// ------------------------------------------------------------------ batched, host arrays
+void __ext_sora_fft64_batch(struct complex16* out, int outlen, struct complex16* in, int inlen) {
+  if (inlen <= 0 || inlen % 64 || outlen < inlen) {
+    std::fprintf(stderr, "ziria_rx: __ext_sora_fft64_batch needs inlen = 64*k and outlen >= inlen\n");
+    return;
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  zrx_ctx* c = default_ctx();
+  const size_t bytes = (size_t)inlen * 4;
+  uint8_t* d = (uint8_t*)staging(c, 2 * bytes);
+  if (!d) ZRX_DIE("staging allocation failed");
+  ZRX_OR_DIE(hipMemcpyAsync(d, in, bytes, hipMemcpyHostToDevice, c->stream));
+  if (zrx_fft64_dev(c, (const complex16*)d, (complex16*)(d + bytes), inlen / 64) != ZRX_OK) ZRX_DIE("fft launch");
+  ZRX_OR_DIE(hipMemcpyAsync(out, d + bytes, bytes, hipMemcpyDeviceToHost, c->stream));
+  ZRX_OR_DIE(hipStreamSynchronize(c->stream));
+}
+
+int32_t __ext_viterbi_batch_decode(int8_t* soft, int softlen, int32_t* pkt_soft_off, int n_off,
+                                   int32_t* frame_len, int n_fl, int16_t* code_rate, int n_cr,
+                                   unsigned char* out_bits, int out_len_bits, int32_t* pkt_out_off, int n_oo) {
+  const int np = n_off - 1;
+  if (np < 0 || n_fl < np || n_cr < np || n_oo < np || softlen < 0 || out_len_bits < 0) return ZRX_EINVAL;
+  if (np == 0) return 0;
+  const int64_t out_bytes = out_len_bits / 8;
+  std::vector<int32_t> params(4 * (size_t)np);
+  std::vector<int64_t> soff(np), ooff(np);
+  for (int i = 0; i < np; i++) {
+    const int32_t n = pkt_soft_off[i + 1] - pkt_soft_off[i];
+    const int cr = code_rate[i];
+    if (cr < 0 || cr > 2 || n < 0 || n % 48 || pkt_soft_off[i] < 0 || pkt_soft_off[i + 1] > softlen ||
+        frame_len[i] < 0 || frame_len[i] > 4990 || pkt_out_off[i] < 0 || pkt_out_off[i] + (int64_t)frame_len[i] > out_bytes)
+      return ZRX_EINVAL;
+    params[4 * i] = frame_len[i]; params[4 * i + 1] = cr; params[4 * i + 2] = n; params[4 * i + 3] = 0;
+    soff[i] = pkt_soft_off[i];
+    ooff[i] = pkt_out_off[i];
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  zrx_ctx* c = default_ctx();
+  const size_t s_soft = ((size_t)softlen + 255) / 256 * 256, s_par = (size_t)np * 16, s_off = (size_t)np * 8;
+  const size_t s_out = ((size_t)out_bytes + 255) / 256 * 256;
+  uint8_t* d = (uint8_t*)staging(c, s_soft + s_par + 2 * s_off + s_out + (size_t)np * 4 + 1024);
+  if (!d) return ZRX_ENOMEM;
+  uint8_t* d_soft = d;
+  int32_t* d_par = (int32_t*)(d_soft + s_soft);
+  int64_t* d_soff = (int64_t*)((uint8_t*)d_par + ((s_par + 255) / 256) * 256);
+  int64_t* d_ooff = (int64_t*)((uint8_t*)d_soff + ((s_off + 255) / 256) * 256);
+  uint8_t* d_out = (uint8_t*)d_ooff + ((s_off + 255) / 256) * 256;
+  int32_t* d_bits = (int32_t*)(d_out + s_out);
+  ZRX_CHECK(hipMemcpyAsync(d_soft, soft, (size_t)softlen, hipMemcpyHostToDevice, c->stream));
+  ZRX_CHECK(hipMemcpyAsync(d_par, params.data(), s_par, hipMemcpyHostToDevice, c->stream));
+  ZRX_CHECK(hipMemcpyAsync(d_soff, soff.data(), s_off, hipMemcpyHostToDevice, c->stream));
+  ZRX_CHECK(hipMemcpyAsync(d_ooff, ooff.data(), s_off, hipMemcpyHostToDevice, c->stream));
+  ZRX_CHECK(hipMemcpyAsync(d_out, out_bits, (size_t)out_bytes, hipMemcpyHostToDevice, c->stream));
+  int rc = zrx_viterbi_dev(c, (const int8_t*)d_soft, d_soff, d_par, np, d_out, d_ooff, d_bits);
+  if (rc) return rc;
+  ZRX_CHECK(hipMemcpyAsync(out_bits, d_out, (size_t)out_bytes, hipMemcpyDeviceToHost, c->stream));
+  ZRX_CHECK(hipStreamSynchronize(c->stream));
+  return np;
+}
+
+int32_t __ext_wifi_rx_batch(struct complex16* sym, int nsym_total, int32_t* pkt_sym_off, int n_off,
+                            unsigned char* payload, int payload_len_bits, int32_t* pkt_info, int n_info) {
+  const int np = n_off - 1;
+  if (np < 0 || nsym_total < 0 || n_info < 8 * np || (int64_t)payload_len_bits / 8 < (int64_t)np * kPayloadStride)
+    return ZRX_EINVAL;
+  if (np == 0) return 0;
+  std::vector<int64_t> off(np);
+  std::vector<int32_t> ns(np);
+  int max_ns = 1;
+  for (int i = 0; i < np; i++) {
+    if (pkt_sym_off[i] < 0 || pkt_sym_off[i + 1] < pkt_sym_off[i] || pkt_sym_off[i + 1] > nsym_total) return ZRX_EINVAL;
+    off[i] = pkt_sym_off[i];
+    ns[i] = pkt_sym_off[i + 1] - pkt_sym_off[i];
+    max_ns = std::max(max_ns, ns[i]);
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  zrx_ctx* c = default_ctx();
+  int rc = zrx_reserve(c, np, max_ns);
+  if (rc) return rc;
+  const size_t s_sym = ((size_t)nsym_total * 256 + 255) / 256 * 256 + 256;
+  const size_t s_off = ((size_t)np * 8 + 255) / 256 * 256, s_ns = ((size_t)np * 4 + 255) / 256 * 256;
+  const size_t s_pay = (size_t)np * kPayloadStride, s_info = (size_t)np * 32;
+  uint8_t* d = (uint8_t*)staging(c, s_sym + s_off + s_ns + s_pay + s_info + 1024);
+  if (!d) return ZRX_ENOMEM;
+  uint8_t* d_sym = d;
+  int64_t* d_off = (int64_t*)(d + s_sym);
+  int32_t* d_ns = (int32_t*)((uint8_t*)d_off + s_off);
+  uint8_t* d_pay = (uint8_t*)d_ns + s_ns;
+  int32_t* d_info = (int32_t*)(d_pay + s_pay);
+  ZRX_CHECK(hipMemcpyAsync(d_sym, sym, (size_t)nsym_total * 256, hipMemcpyHostToDevice, c->stream));
+  ZRX_CHECK(hipMemcpyAsync(d_off, off.data(), (size_t)np * 8, hipMemcpyHostToDevice, c->stream));
+  ZRX_CHECK(hipMemcpyAsync(d_ns, ns.data(), (size_t)np * 4, hipMemcpyHostToDevice, c->stream));
+  ZRX_CHECK(hipMemsetAsync(d_pay, 0, s_pay, c->stream));
+  rc = zrx_rx_dev(c, (const complex16*)d_sym, d_off, d_ns, np, max_ns, d_pay, d_info);
+  if (rc) return rc;
+  ZRX_CHECK(hipMemcpyAsync(payload, d_pay, s_pay, hipMemcpyDeviceToHost, c->stream));
+  ZRX_CHECK(hipMemcpyAsync(pkt_info, d_info, s_info, hipMemcpyDeviceToHost, c->stream));
+  ZRX_CHECK(hipStreamSynchronize(c->stream));
+  int ok = 0;
+  for (int i = 0; i < np; i++) ok += pkt_info[8 * i + 4] != 0;
+  return ok;
+}
+
+}  // extern "C"

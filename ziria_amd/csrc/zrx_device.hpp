@@ -1,0 +1,237 @@
+// Device building blocks of the MI355X 802.11a RX engine (gfx950, wave64).
+//
+// Bit-exactness contract: every routine reproduces the reference bricks' integer
+// semantics exactly (SSE2 saturating int16 adds, XOR-as-negate, madd_epi16 32-bit wrap,
+// u8 wrapping Viterbi metrics with the survivor marker in the metric LSB, signed-int16
+// traceback key).  Reference lines are cited per routine (paths relative to moxfun/Ziria).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "zrx_tables.h"
+
+namespace zrx {
+
+typedef short s2 __attribute__((ext_vector_type(2)));   // one complex16 = (re, im)
+
+__device__ __forceinline__ s2 as_s2(uint32_t v) { return __builtin_bit_cast(s2, v); }
+__device__ __forceinline__ uint32_t as_u32(s2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+// ------------------------------------------------------------------ FFT64 (lane = symbol)
+// _mm_adds_epi16 / _mm_subs_epi16 -> v_pk_add_i16 / v_pk_sub_i16 with clamp.
+__device__ __forceinline__ s2 sat_add(s2 a, s2 b) { return __builtin_elementwise_add_sat(a, b); }
+__device__ __forceinline__ s2 sat_sub(s2 a, s2 b) { return __builtin_elementwise_sub_sat(a, b); }
+__device__ __forceinline__ s2 shr2(s2 a) { return a >> (s2){2, 2}; }               // srai 2
+// mul_jx (csrc/sora_ext_lib_fft.hpp:98-108): (re, im) -> (~im, re)
+__device__ __forceinline__ s2 mul_j(s2 a) { return (s2){(short)~a.y, a.x}; }
+// mul_shiftx(a, b, 15) (csrc/sora_ext_lib_fft.hpp:42-67): madd_epi16 = v_dot2 (32-bit
+// wrapping sum of two exact products), srai 15, low 16 bits.
+__device__ __forceinline__ s2 mul_shift(s2 a, short bre, short bim) {
+  const s2 c1 = {bre, (short)~bim}, c2 = {bim, bre};
+  const int re = __builtin_amdgcn_sdot2(a, c1, 0, false);
+  const int im = __builtin_amdgcn_sdot2(a, c2, 0, false);
+  return (s2){(short)(re >> 15), (short)(im >> 15)};
+}
+
+// FFTSSE<N> (csrc/fft_r4difx.hpp:54-97): one radix-4 DIF stage in place.
+template <int N>
+__device__ __forceinline__ void fft_stage(s2* x) {
+  const int16_t* t1 = N == 64 ? kTw64_1 : kTw16_1;
+  const int16_t* t2 = N == 64 ? kTw64_2 : kTw16_2;
+  const int16_t* t3 = N == 64 ? kTw64_3 : kTw16_3;
+#pragma unroll
+  for (int n = 0; n < N / 4; n++) {
+    const s2 a = shr2(x[n]), b = shr2(x[n + N / 4]), c = shr2(x[n + N / 2]), d = shr2(x[n + 3 * N / 4]);
+    const s2 ac = sat_add(a, c), bd = sat_add(b, d), a_c = sat_sub(a, c), b_d = sat_sub(b, d);
+    x[n] = sat_add(ac, bd);
+    x[n + N / 4] = mul_shift(sat_sub(ac, bd), t2[2 * n], t2[2 * n + 1]);
+    const s2 jb = mul_j(b_d);
+    x[n + N / 2] = mul_shift(sat_sub(a_c, jb), t1[2 * n], t1[2 * n + 1]);
+    x[n + 3 * N / 4] = mul_shift(sat_add(a_c, jb), t3[2 * n], t3[2 * n + 1]);
+  }
+}
+// FFTSSEEx<4> (csrc/fft_r4difx.hpp:111-140), regrouped on packed (re, im) pairs:
+// A = y0+y2, B = y1+y3, L = y0+~y2, T = y1+~y3 (saturating); outputs A+B, ~B+A,
+// L+~j(T), L+j(T) — identical lane-for-lane to the XOR/shuffle sequence.
+__device__ __forceinline__ void fft4(s2* x) {
+  const s2 y0 = shr2(x[0]), y1 = shr2(x[1]), y2 = shr2(x[2]), y3 = shr2(x[3]);
+  const s2 A = sat_add(y0, y2), B = sat_add(y1, y3);
+  const s2 L = sat_add(y0, ~y2), T = sat_add(y1, ~y3);
+  const s2 jT = mul_j(T);
+  x[0] = sat_add(A, B);
+  x[1] = sat_add(~B, A);
+  x[2] = sat_add(L, ~jT);
+  x[3] = sat_add(L, jT);
+}
+__host__ __device__ constexpr int bitrev6(int i) {
+  return ((i & 1) << 5) | ((i & 2) << 3) | ((i & 4) << 1) | ((i & 8) >> 1) | ((i & 16) >> 3) | ((i & 32) >> 5);
+}
+// FFTSSEEx<64> in place; natural-order output bin k lives at x[bitrev6(k)]
+// (bFFT64LUTMap, csrc/sora_ext_lib_fft_coeffs.hpp:15090-15094).
+__device__ __forceinline__ void fft64_inplace(s2* x) {
+  fft_stage<64>(x);
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    fft_stage<16>(x + 16 * q);
+#pragma unroll
+    for (int r = 0; r < 4; r++) fft4(x + 16 * q + 4 * r);
+  }
+}
+
+// ------------------------------------------------------------------ GetData + demap + deinterleave
+// GetData.blk:24-35: data bins 38..42, 44..56, 58..63, 1..6, 8..20, 22..26
+__host__ __device__ constexpr int data_bin(int i) {
+  return i < 5 ? 38 + i : i < 18 ? 44 + (i - 5) : i < 24 ? 58 + (i - 18) : i < 30 ? 1 + (i - 24)
+       : i < 43 ? 8 + (i - 30) : 22 + (i - 43);
+}
+template <int MOD> struct ModInfo;
+template <> struct ModInfo<0> { static constexpr int nb = 1, ncbps = 48; };
+template <> struct ModInfo<1> { static constexpr int nb = 2, ncbps = 96; };
+template <> struct ModInfo<2> { static constexpr int nb = 4, ncbps = 192; };
+template <> struct ModInfo<3> { static constexpr int nb = 6, ncbps = 288; };
+template <int MOD>
+__host__ __device__ constexpr int deint_src(int k) {
+  return MOD == 0 ? kDeint48[k] : MOD == 1 ? kDeint96[k] : MOD == 2 ? kDeint192[k] : kDeint288[k];
+}
+// Demap*.blk:22-33 soft order per subcarrier -> (component 0 = re / 1 = im, LUT byte).
+// LUT bytes: 0 m_bpsk_lut, 1 m_qam16_lut2, 2 m_qam64_lut2, 3 m_qam64_lut3.
+template <int MOD>
+__host__ __device__ constexpr int soft_comp(int c) {
+  return MOD == 0 ? 0 : MOD == 1 ? c : MOD == 2 ? (c >> 1) : (c >= 3 ? 1 : 0);
+}
+template <int MOD>
+__host__ __device__ constexpr int soft_lutbyte(int c) {
+  return MOD <= 1 ? 0 : MOD == 2 ? (c & 1) : (c % 3 == 0 ? 0 : (c % 3 == 1 ? 2 : 3));
+}
+
+// DemapLimit (DemapLimit.blk:22-63, shift 0): clip to [-128,127]; the u8 LUT index is the
+// low byte of the clipped value.  lut: kDemapLut staged in LDS.
+// Writes ncbps soft bytes (deinterleaved, Deinterleave*.blk) as ncbps/4 words.
+template <int MOD>
+__device__ __forceinline__ void demap_deinterleave(const s2* x, const uint32_t* lut, uint32_t* w) {
+  constexpr int NB = ModInfo<MOD>::nb, NC = ModInfo<MOD>::ncbps;
+  uint32_t lr[48], li[48];
+#pragma unroll
+  for (int i = 0; i < 48; i++) {
+    s2 v = x[bitrev6(data_bin(i))];
+    v = __builtin_elementwise_max(__builtin_elementwise_min(v, (s2){127, 127}), (s2){-128, -128});
+    const uint32_t u = as_u32(v);
+    lr[i] = lut[u & 0xFF];
+    li[i] = (MOD == 0) ? 0u : lut[(u >> 16) & 0xFF];
+  }
+#pragma unroll
+  for (int d = 0; d < NC / 4; d++) {
+    uint32_t word = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const int j = deint_src<MOD>(4 * d + b);
+      const int i = j / NB, c = j % NB;
+      const uint32_t src = soft_comp<MOD>(c) ? li[i] : lr[i];
+      word |= ((src >> (8 * soft_lutbyte<MOD>(c))) & 0xFFu) << (8 * b);
+    }
+    w[d] = word;
+  }
+}
+
+// ------------------------------------------------------------------ wave reductions
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
+  return v;
+}
+__device__ __forceinline__ int wave_min_i32(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_xor_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v ^= (uint32_t)__shfl_xor((int)v, o);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o);
+  return v;
+}
+
+// ------------------------------------------------------------------ Viterbi (lane = state)
+// State s = lane.  Predecessors p0 = s>>1 (branch 0, marker 0) and p1 = p0|32 (branch 1,
+// marker 1); input bit x = s&1.  Expected code bits (encoding.blk:92-109):
+// A = x^p1^p2^p4^p5, B = x^p0^p1^p2^p5; branch metric e ? 14-2v : 2v reproduces
+// VIT_MA/VIT_MB (csrc/viterbilut.h:111-285); branch 1 expects the complement bits, so
+// its metric is (28 or 14) - branch 0's.
+struct VitLane {
+  int cA, offA, cB, offB;   // bm0 = cA*2a + offA (+ cB*2b + offB)
+  int src0, src1;           // predecessor lanes
+};
+__device__ __forceinline__ VitLane vit_lane(int s) {
+  const int p0 = s >> 1, x = s & 1;
+  const int A = x ^ ((p0 >> 1) & 1) ^ ((p0 >> 2) & 1) ^ ((p0 >> 4) & 1) ^ ((p0 >> 5) & 1);
+  const int B = x ^ (p0 & 1) ^ ((p0 >> 1) & 1) ^ ((p0 >> 2) & 1) ^ ((p0 >> 5) & 1);
+  VitLane L;
+  L.cA = 1 - 2 * A; L.offA = 14 * A;
+  L.cB = 1 - 2 * B; L.offB = 14 * B;
+  L.src0 = p0; L.src1 = p0 | 32;
+  return L;
+}
+// One trellis column: BranchACS (csrc/viterbicore.hpp:105-147, 241-265, 343-390).
+// USE: 3 = (a on A, b on B), 1 = a on A only, 2 = a on B only.  m holds a u8 metric.
+template <int USE>
+__device__ __forceinline__ uint32_t acs(uint32_t m, int a, int b, const VitLane& L) {
+  const uint32_t m0 = (uint32_t)__shfl((int)m, L.src0);
+  const uint32_t m1 = (uint32_t)__shfl((int)m, L.src1);
+  int bm0, tot;
+  if (USE == 3) { bm0 = L.cA * (2 * a) + L.offA + L.cB * (2 * b) + L.offB; tot = 28; }
+  else if (USE == 1) { bm0 = L.cA * (2 * a) + L.offA; tot = 14; }
+  else { bm0 = L.cB * (2 * a) + L.offB; tot = 14; }
+  const uint32_t r0 = (m0 + (uint32_t)bm0) & 0xFEu;                 // add_epi8, AND 0xFE
+  const uint32_t r1 = ((m1 + (uint32_t)(tot - bm0)) & 0xFFu) | 1u;  // add_epi8, OR 1
+  return min(r0, r1);                                                // min_epu8
+}
+// normalize (csrc/viterbicore.hpp:149-168)
+__device__ __forceinline__ uint32_t vit_normalize(uint32_t m) {
+  return m - (wave_min_u32(m) & 0xFEu);
+}
+// traceback (csrc/viterbicore.hpp:170-239).  Start = argmin of the SIGNED int16 key
+// (m<<8)|(4s) (SSE2 hmin16, :79-96); the state's own survivor bit rides in bit 6.
+// surv(t) returns the 64-bit survivor word of column t (bit s = LSB of m_t[s]).
+// Returns, in lane j, output byte j (bytes 0 .. nbits/8-1 in stream order).
+template <class SurvRead>
+__device__ __forceinline__ uint32_t vit_traceback(uint32_t m, uint32_t col, uint32_t nbits,
+                                                  uint32_t lookahead, int lane, SurvRead surv) {
+  int key = (int)(int16_t)(uint16_t)((m << 8) | ((uint32_t)lane << 2));
+  key = wave_min_i32(key);
+  uint32_t i = (uint32_t)(key >> 2) & 0x7Fu;
+  uint32_t t = col;
+  for (uint32_t k = 0; k < lookahead; k++) {
+    t--;
+    i = (i >> 1) & 0x3Fu;
+    i |= (uint32_t)((surv(t) >> i) & 1u) << 6;
+  }
+  const int nbytes = (int)(nbits >> 3);
+  uint32_t mine = 0;
+  for (int byte = nbytes - 1; byte >= 0; byte--) {
+    uint32_t oc = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      oc = (oc << 1) | ((i >> 6) & 1u);
+      t--;
+      i = (i >> 1) & 0x3Fu;
+      i |= (uint32_t)((surv(t) >> i) & 1u) << 6;
+    }
+    if (lane == byte) mine = oc;
+  }
+  return mine;
+}
+
+// ------------------------------------------------------------------ descrambler / CRC helpers
+// CRC register after processing n zero bytes (linear map), via kCrcZero[k] = 2^k bytes.
+__device__ __forceinline__ uint32_t crc_apply(const uint32_t* M, uint32_t v) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < 32; i++) r ^= ((v >> i) & 1u) ? M[i] : 0u;
+  return r;
+}
+
+}  // namespace zrx

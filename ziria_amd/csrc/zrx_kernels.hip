@@ -1,0 +1,435 @@
+// MI355X (gfx950) kernels of the 802.11a RX decode hot path.
+//
+//   k_fft64          one 64-point FFT per lane (FFT<64>, csrc/fft_r4difx.hpp:220-237)
+//   k_signal_fft     SIGNAL symbol per lane: FFT -> GetData -> DemapLimit -> DemapBPSK ->
+//                    DeinterleaveBPSK (DecodePLCP.blk:30-37)
+//   k_signal_vit     one wave per packet: Viterbi_sig11 (viterbicore.hpp:272-315) +
+//                    parsePLCPHeader (parsePLCPHeader.blk:119-213)
+//   k_data_fft       one wave per packet, lane = data symbol: FFT -> GetData -> DemapLimit ->
+//                    Demap{mod} -> Deinterleave{mod} (Decode.blk:45-60)
+//   k_viterbi        one wave per packet, lane = trellis state: the whole brick driver loop
+//                    (sora_ext_viterbi.cpp:66-153) with the survivor history in an LDS ring
+//   k_descramble_crc one wave per packet: descrambler (Decode.blk:36-43) + CRC-32 check
+//                    (crc.blk:85-118), 64 lanes each on a chunk, CRC combined by GF(2) maps
+//   k_viterbi_stream / k_vit_init / k_sig_bytes / k_shift_right: the per-call externals.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "zrx_device.hpp"
+
+namespace zrx {
+
+constexpr int kRing = 512;            // survivor ring columns per packet (>= depth + 64)
+constexpr int kDecStride = 2080;      // decoded bytes per packet in the rx chain (len+2 <= 2050)
+constexpr int kPayloadStride = 4096;  // payload bytes per packet
+
+// ------------------------------------------------------------------ FFT64 batch
+__global__ __launch_bounds__(256) void k_fft64(const uint4* __restrict__ in, uint4* __restrict__ out,
+                                               int64_t nsym) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsym) return;
+  s2 x[64];
+  const uint4* src = in + s * 16;
+#pragma unroll
+  for (int q = 0; q < 16; q++) {
+    const uint4 v = src[q];
+    x[4 * q] = as_s2(v.x); x[4 * q + 1] = as_s2(v.y); x[4 * q + 2] = as_s2(v.z); x[4 * q + 3] = as_s2(v.w);
+  }
+  fft64_inplace(x);
+  uint4* dst = out + s * 16;
+#pragma unroll
+  for (int q = 0; q < 16; q++) {
+    dst[q] = make_uint4(as_u32(x[bitrev6(4 * q)]), as_u32(x[bitrev6(4 * q + 1)]),
+                        as_u32(x[bitrev6(4 * q + 2)]), as_u32(x[bitrev6(4 * q + 3)]));
+  }
+}
+
+__device__ __forceinline__ void load_symbol(const uint4* __restrict__ src, s2* x) {
+#pragma unroll
+  for (int q = 0; q < 16; q++) {
+    const uint4 v = src[q];
+    x[4 * q] = as_s2(v.x); x[4 * q + 1] = as_s2(v.y); x[4 * q + 2] = as_s2(v.z); x[4 * q + 3] = as_s2(v.w);
+  }
+}
+
+__device__ __forceinline__ void stage_lut(uint32_t* lut) {
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) lut[i] = kDemapLut[i];
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------ SIGNAL symbol -> 48 soft
+__global__ __launch_bounds__(256) void k_signal_fft(const uint4* __restrict__ sym, const int64_t* __restrict__ sym_off,
+                                                    const int32_t* __restrict__ nsym, int npkts,
+                                                    uint4* __restrict__ sig_soft) {
+  __shared__ uint32_t lut[256];
+  stage_lut(lut);
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npkts) return;
+  uint32_t w[12];
+  if (nsym[p] >= 1) {
+    s2 x[64];
+    load_symbol(sym + sym_off[p] * 16, x);
+    fft64_inplace(x);
+    demap_deinterleave<0>(x, lut, w);
+  } else {
+#pragma unroll
+    for (int d = 0; d < 12; d++) w[d] = 0;
+  }
+  uint4* dst = sig_soft + (int64_t)p * 3;
+  dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  dst[2] = make_uint4(w[8], w[9], w[10], w[11]);
+}
+
+// ------------------------------------------------------------------ Viterbi core (one wave)
+struct RingLds {
+  uint64_t* r;
+  __device__ __forceinline__ uint64_t operator()(uint32_t t) const { return r[t & (kRing - 1)]; }
+};
+
+// Viterbi_sig11: 24 full steps on 48 soft values held as 12 dwords in lanes 0..11 of `dw`.
+// Returns (in lane j) traceback byte j of the 3 output bytes (before the >>6 of :191).
+__device__ __forceinline__ uint32_t sig11_bytes(uint32_t dw, int lane, uint64_t* ring) {
+  const VitLane L = vit_lane(lane);
+  uint32_t m = lane == 0 ? 0u : 48u;
+  if (lane == 0) ring[0] = 0;
+#pragma unroll
+  for (int t = 1; t <= 24; t++) {
+    const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)dw, (2 * t - 2) >> 2);
+    const int sh = ((2 * t - 2) & 3) * 8;
+    const int a = (word >> sh) & 0xFF, b = (word >> (sh + 8)) & 0xFF;
+    m = acs<3>(m, a, b, L);
+    if ((t & 7) == 0) m = vit_normalize(m);
+    const uint64_t w = __ballot((m & 1u) != 0);
+    if (lane == 0) ring[t] = w;
+  }
+  m = vit_normalize(m);
+  return vit_traceback(m, 24u, 24u, 0u, lane, RingLds{ring});
+}
+
+__device__ __forceinline__ int ncbps_of(int mod) { return mod == 0 ? 48 : mod == 1 ? 96 : mod == 2 ? 192 : 288; }
+// N_DBPS (transmitter.blk:39-46)
+__device__ __forceinline__ int ndbps_of(int mod, int coding) {
+  const int nc = ncbps_of(mod);
+  return coding == 0 ? nc / 2 : coding == 1 ? nc * 2 / 3 : nc * 3 / 4;
+}
+
+// SIGNAL Viterbi + parsePLCPHeader -> Viterbi/FFT parameters and packet info.
+// vparams[4p..] = {frame_len, code_rate, soft_len, modulation}
+// info[8p..]    = {modulation, coding, len, header_err, crc_ok, status, symbols_used, viterbi_bits}
+__global__ __launch_bounds__(256) void k_signal_vit(const uint32_t* __restrict__ sig_soft, const int32_t* __restrict__ nsym,
+                                                    int npkts, int32_t* __restrict__ vparams,
+                                                    int32_t* __restrict__ info) {
+  __shared__ uint64_t ring_all[4][32];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int p = blockIdx.x * 4 + wv;
+  if (p >= npkts) return;
+  const uint32_t dw = lane < 12 ? sig_soft[(int64_t)p * 12 + lane] : 0u;
+  const uint32_t byte = sig11_bytes(dw, lane, ring_all[wv]);
+  const uint32_t b0 = __builtin_amdgcn_readlane((int)byte, 0);
+  const uint32_t b1 = __builtin_amdgcn_readlane((int)byte, 1);
+  const uint32_t b2 = __builtin_amdgcn_readlane((int)byte, 2);
+  const uint32_t hb = ((b0 | (b1 << 8) | (b2 << 16)) >> 6) & 0x3FFFFu;   // bits 18..23 := 0
+  // parsePLCPHeader.blk:124-158 RATE nibble (bit k of the nibble = hdata[k])
+  int mod = 0, cod = 0;
+  switch (hb & 0xF) {
+    case 0xB: mod = 0; cod = 0; break;
+    case 0xF: mod = 0; cod = 2; break;
+    case 0xA: mod = 1; cod = 0; break;
+    case 0xE: mod = 1; cod = 2; break;
+    case 0x9: mod = 2; cod = 0; break;
+    case 0xD: mod = 2; cod = 2; break;
+    case 0x8: mod = 3; cod = 1; break;
+    case 0xC: mod = 3; cod = 2; break;
+    default: mod = 0; cod = 0;
+  }
+  int len = (int)((hb >> 5) & 0xFFF);
+  int err = 0;
+  if (len > 2048) { err = 1; len = 2048; }            // :171-174
+  if (__builtin_popcount(hb) & 1) err = 1;            // parity over 24 bits (:177-188)
+  const int nd = ndbps_of(mod, cod);
+  const int need = (16 + 8 * len + 6 + nd - 1) / nd;  // symbols holding SERVICE .. tail
+  int status = 0;
+  if (err) status = 1;
+  else if (need > nsym[p] - 1) status = 2;
+  if (lane == 0) {
+    int32_t* vp = vparams + 4 * (int64_t)p;
+    vp[0] = len + 2;                                  // Decode.blk:59 Viterbi(h.coding, h.len+2)
+    vp[1] = cod;
+    vp[2] = status == 0 ? need * ncbps_of(mod) : 0;
+    vp[3] = mod;
+    int32_t* in = info + 8 * (int64_t)p;
+    in[0] = mod; in[1] = cod; in[2] = len; in[3] = err; in[4] = 0; in[5] = status;
+    in[6] = 1 + (status == 0 ? need : 0); in[7] = 0;
+  }
+}
+
+// ------------------------------------------------------------------ data symbols -> soft
+template <int MOD>
+__device__ __forceinline__ void data_fft_packet(const uint4* __restrict__ sym0, int need, int lane,
+                                                const uint32_t* lut, uint4* __restrict__ dst0) {
+  constexpr int NC = ModInfo<MOD>::ncbps;
+  for (int k = lane; k < need; k += 64) {
+    s2 x[64];
+    load_symbol(sym0 + (int64_t)k * 16, x);
+    fft64_inplace(x);
+    uint32_t w[NC / 4];
+    demap_deinterleave<MOD>(x, lut, w);
+    uint4* dst = dst0 + (int64_t)k * (NC / 16);
+#pragma unroll
+    for (int q = 0; q < NC / 16; q++) dst[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+  }
+}
+__global__ __launch_bounds__(256) void k_data_fft(const uint4* __restrict__ sym, const int64_t* __restrict__ sym_off,
+                                                  const int32_t* __restrict__ vparams, int npkts,
+                                                  uint4* __restrict__ soft, const int64_t* __restrict__ soft_off) {
+  __shared__ uint32_t lut[256];
+  stage_lut(lut);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int p = blockIdx.x * 4 + wv;
+  if (p >= npkts) return;
+  const int32_t* vp = vparams + 4 * (int64_t)p;
+  const int soft_len = vp[2], mod = vp[3];
+  if (soft_len <= 0) return;
+  const uint4* s0 = sym + (sym_off[p] + 1) * 16;
+  uint4* d0 = soft + soft_off[p] / 16;
+  switch (mod) {
+    case 0: data_fft_packet<0>(s0, soft_len / 48, lane, lut, d0); break;
+    case 1: data_fft_packet<1>(s0, soft_len / 96, lane, lut, d0); break;
+    case 2: data_fft_packet<2>(s0, soft_len / 192, lane, lut, d0); break;
+    default: data_fft_packet<3>(s0, soft_len / 288, lane, lut, d0); break;
+  }
+}
+
+// ------------------------------------------------------------------ Viterbi brick, batched
+// Decoder state of the brick driver loop (sora_ext_viterbi.cpp:66-153) for one packet.
+struct VitRun {
+  uint32_t m, tr, ob, total_bytes, tr_end, depth;
+  bool done;
+};
+
+// Post-group bookkeeping: normalize (:112-116) and the traceback schedule (:118-149).
+template <class Surv>
+__device__ __forceinline__ void vit_after_group(VitRun& v, int lane, Surv surv, uint8_t* __restrict__ out) {
+  if ((v.tr & 7u) == 0) v.m = vit_normalize(v.m);
+  uint32_t cnt = 0, look = 0;
+  if (v.tr >= v.tr_end) {
+    cnt = v.tr_end - v.ob - 6u;
+    look = v.tr - v.tr_end;
+    v.done = true;                                  // nothing can be output afterwards
+  } else if (v.tr >= v.ob + v.depth + 30u) {
+    cnt = v.depth;
+    look = 24u + (v.tr - (v.ob + v.depth + 30u)) % 8u;
+  }
+  if (cnt) {
+    const uint32_t byte = vit_traceback(v.m, v.tr, cnt, look, lane, surv);
+    const uint32_t nb = cnt >> 3;
+    if ((uint32_t)lane < nb) out[v.total_bytes + lane] = (uint8_t)byte;
+    v.ob += cnt;
+    v.total_bytes += nb;
+  }
+}
+
+template <int USE>
+__device__ __forceinline__ void vit_step(VitRun& v, int a, int b, const VitLane& L, int lane, uint64_t* ring) {
+  v.m = acs<USE>(v.m, a, b, L);
+  v.tr++;
+  const uint64_t w = __ballot((v.m & 1u) != 0);
+  if (lane == 0) ring[v.tr & (kRing - 1)] = w;
+}
+
+// Runs all groups of one packet.  Soft values are read 192 at a time (48 dwords, one per
+// lane) and broadcast with readlane; 192 is a multiple of every group size (2, 3, 4).
+template <int CR>
+__device__ __forceinline__ void vit_packet(const uint8_t* __restrict__ sp, int n, VitRun& v, const VitLane& L,
+                                           int lane, uint64_t* ring, uint8_t* __restrict__ out) {
+  constexpr int G = CR == 0 ? 2 : (CR == 1 ? 3 : 4);
+  for (int base = 0; base < n && !v.done; base += 192) {
+    const uint32_t chunk = (lane < 48 && base + 4 * lane < n) ? *(const uint32_t*)(sp + base + 4 * lane) : 0u;
+    const int cn = min(192, n - base);
+    for (int k = 0; k < cn && !v.done; k += 12) {
+      const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)chunk, k >> 2);
+      const uint32_t d1 = (uint32_t)__builtin_amdgcn_readlane((int)chunk, (k >> 2) + 1);
+      const uint32_t d2 = (uint32_t)__builtin_amdgcn_readlane((int)chunk, (k >> 2) + 2);
+      int s[12];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        s[q] = (d0 >> (8 * q)) & 0xFF; s[4 + q] = (d1 >> (8 * q)) & 0xFF; s[8 + q] = (d2 >> (8 * q)) & 0xFF;
+      }
+#pragma unroll
+      for (int g = 0; g < 12 / G; g++) {
+        if (v.done) break;
+        const int* q = s + g * G;
+        vit_step<3>(v, q[0], q[1], L, lane, ring);
+        if (CR == 2) { vit_step<1>(v, q[2], 0, L, lane, ring); vit_step<2>(v, q[3], 0, L, lane, ring); }
+        if (CR == 1) { vit_step<1>(v, q[2], 0, L, lane, ring); }
+        vit_after_group(v, lane, RingLds{ring}, out);
+      }
+    }
+  }
+}
+
+// vparams[4p..] = {frame_len, code_rate, soft_len, *}; out_bits[p] = bits written.
+__global__ __launch_bounds__(256) void k_viterbi(const uint8_t* __restrict__ soft, const int64_t* __restrict__ soft_off,
+                                                 const int32_t* __restrict__ vparams, int npkts,
+                                                 uint8_t* __restrict__ out, const int64_t* __restrict__ out_off,
+                                                 int32_t* __restrict__ out_bits, int depth) {
+  __shared__ uint64_t ring_all[4][kRing];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int p = blockIdx.x * 4 + wv;
+  if (p >= npkts) return;
+  uint64_t* ring = ring_all[wv];
+  const int32_t* vp = vparams + 4 * (int64_t)p;
+  const int fl = vp[0], cr = vp[1], n = vp[2];
+  VitRun v;
+  v.m = lane == 0 ? 0u : 48u;                       // ALL_INIT0 / ALL_INIT (viterbilut.h:74-82)
+  v.tr = 0; v.ob = 0; v.total_bytes = 0;
+  v.tr_end = (uint32_t)fl * 8u + 6u; v.depth = (uint32_t)depth; v.done = false;
+  if (lane == 0) ring[0] = 0;
+  const VitLane L = vit_lane(lane);
+  const uint8_t* sp = soft + soft_off[p];
+  uint8_t* op = out + out_off[p];
+  if (n > 0) {
+    if (cr == 0) vit_packet<0>(sp, n, v, L, lane, ring, op);
+    else if (cr == 1) vit_packet<1>(sp, n, v, L, lane, ring, op);
+    else if (cr == 2) vit_packet<2>(sp, n, v, L, lane, ring, op);
+  }
+  if (lane == 0) out_bits[p] = (int32_t)(v.total_bytes * 8u);
+}
+
+// ------------------------------------------------------------------ descramble + CRC
+// info[8p+4] = crc_ok, info[8p+7] = viterbi bits; payload gets len-4 descrambled bytes.
+__global__ __launch_bounds__(256) void k_descramble_crc(const uint8_t* __restrict__ dec, const int32_t* __restrict__ dec_bits,
+                                                        int32_t* __restrict__ info, uint8_t* __restrict__ payload,
+                                                        int npkts) {
+  __shared__ uint32_t crctab[256];
+  __shared__ uint8_t scr[128];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) crctab[i] = kCrcTab[i];
+  for (int i = threadIdx.x; i < 127; i += blockDim.x) scr[i] = kScrByte[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int p = blockIdx.x * 4 + wv;
+  if (p >= npkts) return;
+  int32_t* in = info + 8 * (int64_t)p;
+  const int len = in[2], status = in[5];
+  const int bits = dec_bits[p];
+  if (lane == 0) in[7] = bits;
+  if (status != 0 || bits < (len + 2) * 8 || len < 4) {
+    if (lane == 0) in[4] = 0;
+    return;
+  }
+  const uint8_t* d = dec + (int64_t)p * kDecStride;
+  uint8_t* py = payload + (int64_t)p * kPayloadStride;
+  const uint32_t S = (uint32_t)d[1] >> 1;           // SERVICE bits 9..15 = scrambler state
+  const int ph = kScrPhase[S];
+  const int plen = len - 4;
+  const int c = (len + 63) >> 6;
+  const int lo = lane * c, hi = min(lo + c, len);
+  uint32_t crc = lane == 0 ? 0xFFFFFFFFu : 0u;
+  uint32_t rx = 0;
+  int ks = S == 0 ? 0 : (ph + 8 * lo) % 127;
+  for (int q = lo; q < hi; q++) {
+    const uint32_t kb = S == 0 ? 0u : scr[ks];
+    ks += 8; if (ks >= 127) ks -= 127;
+    const uint32_t b = (uint32_t)d[2 + q] ^ kb;
+    if (q < plen) {
+      py[q] = (uint8_t)b;
+      crc = crctab[(crc ^ b) & 0xFFu] ^ (crc >> 8);
+    } else {
+      rx |= b << (8 * (q - plen));
+    }
+  }
+  // shift this lane's partial register past the bytes that follow its chunk
+  int zeros = plen - min(hi, plen);
+  if (zeros < 0) zeros = 0;
+  for (int k = 0; k < 13; k++)
+    if ((zeros >> k) & 1) crc = crc_apply(kCrcZero[k], crc);
+  crc = wave_xor_u32(crc);
+  rx = wave_or_u32(rx);
+  if (lane == 0) in[4] = (~crc == rx) ? 1 : 0;
+}
+
+// ------------------------------------------------------------------ per-call externals
+// Streaming decoder with the reference's global-brick semantics (sora_ext_viterbi.cpp:39-46):
+// full trellis history (TRELLIS_MAX = 40000 columns) in device memory.
+constexpr int kTrellisMax = 40000;
+struct VitStream {
+  uint32_t m[64];
+  uint32_t tr, ob, frame_len, code_rate, depth, pad[3];
+  uint64_t surv[kTrellisMax + 16];
+};
+__global__ void k_vit_init(VitStream* st, int frame_len, int code_rate, int depth) {
+  const int lane = threadIdx.x;
+  st->m[lane] = lane == 0 ? 0u : 48u;
+  if (lane == 0) {
+    st->tr = 0; st->ob = 0; st->frame_len = (uint32_t)frame_len; st->code_rate = (uint32_t)code_rate;
+    st->depth = (uint32_t)depth; st->surv[0] = 0;
+  }
+}
+struct SurvGlobal {
+  const uint64_t* s;
+  __device__ __forceinline__ uint64_t operator()(uint32_t t) const {
+    return __hip_atomic_load(s + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+};
+template <int USE>
+__device__ __forceinline__ void stream_step(VitRun& v, int a, int b, const VitLane& L, int lane, VitStream* st) {
+  v.m = acs<USE>(v.m, a, b, L);
+  v.tr++;
+  const uint64_t w = __ballot((v.m & 1u) != 0);
+  if (lane == 0 && v.tr < (uint32_t)(kTrellisMax + 16))
+    __hip_atomic_store(st->surv + v.tr, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// One decode call on n soft values (one wave).  out gets this call's bytes; *out_bits its bits.
+__global__ void k_viterbi_stream(VitStream* st, const uint8_t* __restrict__ sp, int n, uint8_t* __restrict__ out,
+                                 int32_t* __restrict__ out_bits) {
+  const int lane = threadIdx.x;
+  const VitLane L = vit_lane(lane);
+  VitRun v;
+  v.m = st->m[lane];
+  v.tr = st->tr; v.ob = st->ob; v.total_bytes = 0;
+  v.tr_end = st->frame_len * 8u + 6u; v.depth = st->depth; v.done = false;
+  const int cr = (int)st->code_rate;
+  const int G = cr == 0 ? 2 : (cr == 1 ? 3 : (cr == 2 ? 4 : 0));
+  if (G) {
+    for (int k = 0; k + G <= n; k += G) {
+      const int a = sp[k], b = sp[k + 1];
+      stream_step<3>(v, a, b, L, lane, st);
+      if (cr == 2) { stream_step<1>(v, sp[k + 2], 0, L, lane, st); stream_step<2>(v, sp[k + 3], 0, L, lane, st); }
+      if (cr == 1) { stream_step<1>(v, sp[k + 2], 0, L, lane, st); }
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+      v.done = false;   // the brick keeps running after the final traceback (output 0 bits)
+      vit_after_group(v, lane, SurvGlobal{st->surv}, out);
+    }
+  }
+  st->m[lane] = v.m;
+  if (lane == 0) { st->tr = v.tr; st->ob = v.ob; *out_bits = (int32_t)(v.total_bytes * 8u); }
+}
+// Viterbi_sig11 for a batch: 3 traceback bytes per packet (before the brick's >>6).
+__global__ __launch_bounds__(256) void k_sig_bytes(const uint32_t* __restrict__ sig_soft, int npkts, uint8_t* __restrict__ out3) {
+  __shared__ uint64_t ring_all[4][32];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int p = blockIdx.x * 4 + wv;
+  if (p >= npkts) return;
+  const uint32_t dw = lane < 12 ? sig_soft[(int64_t)p * 12 + lane] : 0u;
+  const uint32_t byte = sig11_bytes(dw, lane, ring_all[wv]);
+  if (lane < 3) out3[(int64_t)p * 3 + lane] = (uint8_t)byte;
+}
+// __ext_v_shift_right_complex16 (sora_ext_lib.cpp:1979-1995): the first len/4*4 complex
+// values use srai_epi16 (arithmetic); the tail uses unum16 >> shift (logical).
+__global__ void k_shift_right(const uint16_t* __restrict__ x, uint16_t* __restrict__ z, int len, int shift) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= 2 * len) return;
+  const uint16_t v = x[e];
+  uint16_t r;
+  if (e < (len / 4) * 8) {
+    const int16_t sv = (int16_t)v;
+    r = (uint16_t)((shift < 0 || shift > 15) ? (sv < 0 ? -1 : 0) : (sv >> shift));
+  } else {
+    r = (uint16_t)((shift < 0 || shift > 15) ? 0 : (v >> shift));
+  }
+  z[e] = r;
+}
+
+}  // namespace zrx

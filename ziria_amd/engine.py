@@ -1,0 +1,92 @@
+"""Batched decode engine over device-resident (HBM) buffers.
+
+Drives the Part-3 C-ABI of libziria_rx.so (zrx_*) with torch tensors as the device memory
+allocator and torch's current HIP stream as the launch stream; torch is plumbing here, the
+kernels are the hand-written HIP in ziria_amd/csrc.
+"""
+import ctypes as C
+
+import torch
+
+from ._lib import ZiriaRxError, check, lib
+
+PAYLOAD_STRIDE = 4096
+STAGES = ("signal_fft", "signal_viterbi", "data_fft_demap", "data_viterbi", "descramble_crc")
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr())
+
+
+class RxEngine:
+    """One engine context per device.  Methods launch asynchronously on the current stream."""
+
+    def __init__(self, device=0):
+        if not torch.cuda.is_available():
+            raise ZiriaRxError("RxEngine needs a HIP device (no CPU path)")
+        self.device = torch.device("cuda", device)
+        h = C.c_void_p()
+        with torch.cuda.device(self.device):
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            check(lib().zrx_create(C.byref(h), device, C.c_void_p(stream)), "zrx_create")
+        self._h = h
+
+    def close(self):
+        if self._h:
+            lib().zrx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _stream(self):
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        check(lib().zrx_set_stream(self._h, C.c_void_p(s)), "zrx_set_stream")
+
+    def reserve(self, npkts, max_nsym):
+        check(lib().zrx_reserve(self._h, int(npkts), int(max_nsym)), "zrx_reserve")
+
+    def enable_timing(self, on=True):
+        check(lib().zrx_enable_timing(self._h, 1 if on else 0), "zrx_enable_timing")
+
+    def stage_ms(self):
+        ms = (C.c_float * 5)()
+        check(lib().zrx_get_timing(self._h, ms), "zrx_get_timing")
+        return dict(zip(STAGES, [float(v) for v in ms]))
+
+    # ------------------------------------------------------------------ launches
+    def fft64(self, sym, out=None):
+        """sym: int16 [S, 64, 2] on the device -> FFT64 of every symbol."""
+        assert sym.dtype == torch.int16 and sym.is_contiguous() and sym.shape[-2:] == (64, 2)
+        out = torch.empty_like(sym) if out is None else out
+        self._stream()
+        check(lib().zrx_fft64_dev(self._h, _ptr(sym), _ptr(out), sym.numel() // 128), "zrx_fft64_dev")
+        return out
+
+    def viterbi(self, soft, soft_off, params, out, out_off, out_bits):
+        """soft int8, soft_off int64 [n], params int32 [n,4] {frame_len, code_rate,
+        soft_len, 0}, out uint8, out_off int64 [n], out_bits int32 [n] (all on device)."""
+        n = soft_off.numel()
+        for t in (soft, soft_off, params, out, out_off, out_bits):
+            assert t.is_cuda and t.is_contiguous()
+        assert params.dtype == torch.int32 and params.numel() == 4 * n
+        self._stream()
+        check(lib().zrx_viterbi_dev(self._h, _ptr(soft), _ptr(soft_off), _ptr(params), n, _ptr(out),
+                                    _ptr(out_off), _ptr(out_bits)), "zrx_viterbi_dev")
+
+    def rx(self, sym, sym_off, nsym, max_nsym, payload=None, info=None):
+        """Full chain.  sym int16 [S,64,2]; sym_off int64 [n] (SIGNAL symbol index);
+        nsym int32 [n].  Returns (payload uint8 [n,4096], info int32 [n,8])."""
+        n = sym_off.numel()
+        assert sym.dtype == torch.int16 and sym_off.dtype == torch.int64 and nsym.dtype == torch.int32
+        if payload is None:
+            payload = torch.zeros((n, PAYLOAD_STRIDE), dtype=torch.uint8, device=sym.device)
+        if info is None:
+            info = torch.zeros((n, 8), dtype=torch.int32, device=sym.device)
+        self._stream()
+        check(lib().zrx_rx_dev(self._h, _ptr(sym), _ptr(sym_off), _ptr(nsym), n, int(max_nsym),
+                               _ptr(payload), _ptr(info)), "zrx_rx_dev")
+        return payload, info

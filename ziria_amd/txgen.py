@@ -1,0 +1,186 @@
+"""Synthetic 802.11a packet workloads (BASELINE configs 2, 3, 5), vectorized in torch so
+that a 16k-packet batch is generated in seconds (on the GPU when one is present).
+
+This is a workload generator, not part of the decode path.  It restates the transmitter
+(code/WiFi/transmitter/transmitter.blk:56-101: crc + SERVICE + pad, scrambler 1011101,
+encode12/23/34, interleave, modulate) and the channel of SURVEY.md Appendix E:
+x = IDFT(X / 100) * 64 + N(0, sigma^2) per component, rounded to int16.
+tests/test_txgen.py checks it against the oracle's transmitter restatement.
+"""
+import zlib
+
+import numpy as np
+import torch
+
+NCBPS = {0: 48, 1: 96, 2: 192, 3: 288}
+UNIT = {0: 10720, 1: 7581, 2: 3390, 3: 1654}          # const.blk:27-30 (int16 of the quotient)
+DATA_BINS = (list(range(38, 43)) + list(range(44, 57)) + list(range(58, 64)) + list(range(1, 7)) +
+             list(range(8, 21)) + list(range(22, 27)))       # GetData.blk:24-35
+PILOT_BINS = [7, 21, 43, 57]
+RATE_NIBBLE = {(0, 0): 0xB, (0, 2): 0xF, (1, 0): 0xA, (1, 2): 0xE, (2, 0): 0x9, (2, 2): 0xD,
+               (3, 1): 0x8, (3, 2): 0xC}
+
+
+def ndbps(mod, coding):
+    nc = NCBPS[mod]
+    return nc // 2 if coding == 0 else (nc * 2 // 3 if coding == 1 else nc * 3 // 4)
+
+
+def n_data_symbols(mod, coding, payload_len):
+    """Data OFDM symbols for a payload of payload_len bytes (+4 CRC)."""
+    nd = ndbps(mod, coding)
+    return (16 + 8 * payload_len + 32 + 6 + nd - 1) // nd
+
+
+def interleave_perm(mod):
+    """p(k) of the 802.11a interleaver (interleaving.blk:38-58); TX: out[p(k)] = in[k]."""
+    N = NCBPS[mod]
+    s = max(N // 48 // 2, 1)
+    k = np.arange(N)
+    i = (N // 16) * (k % 16) + k // 16
+    return s * (i // s) + (i + N - (16 * i) // N) % s
+
+
+def _scrambler_keystream(n):
+    st = [1, 0, 1, 1, 1, 0, 1]                       # default_scrmbl_st (scramble.blk:22)
+    out = np.zeros(n, np.uint8)
+    for k in range(n):
+        t = st[3] ^ st[0]
+        st = st[1:] + [t]
+        out[k] = t
+    return out
+
+
+def _encode(u, coding):
+    """u: uint8 [n, L] bits -> punctured coded bits (encoding.blk:24-109)."""
+    n, L = u.shape
+    z = torch.zeros((n, 6), dtype=u.dtype, device=u.device)
+    p = torch.cat([z, u], 1)
+    d = lambda k: p[:, 6 - k: 6 - k + L]             # u[n-k]
+    A = d(0) ^ d(2) ^ d(3) ^ d(5) ^ d(6)
+    B = d(0) ^ d(1) ^ d(2) ^ d(3) ^ d(6)
+    if coding == 0:
+        return torch.stack([A, B], 2).reshape(n, 2 * L)
+    if coding == 2:                                  # A0 B0 A1 B2 per 3 input bits
+        A3, B3 = A.reshape(n, L // 3, 3), B.reshape(n, L // 3, 3)
+        return torch.stack([A3[..., 0], B3[..., 0], A3[..., 1], B3[..., 2]], 2).reshape(n, -1)
+    A2, B2 = A.reshape(n, L // 2, 2), B.reshape(n, L // 2, 2)   # 2/3: A0 B0 A1
+    return torch.stack([A2[..., 0], B2[..., 0], A2[..., 1]], 2).reshape(n, -1)
+
+
+def _map(bits, mod):
+    """bits uint8 [..., nbpsc] -> (re, im) levels in units (modulating.blk)."""
+    b = bits.to(torch.int64)
+    if mod == 0:
+        return (2 * b[..., 0] - 1), torch.zeros_like(b[..., 0])
+    if mod == 1:
+        return 2 * b[..., 0] - 1, 2 * b[..., 1] - 1
+    if mod == 2:
+        g = torch.tensor([-3, -1, 3, 1], device=bits.device)
+        return g[2 * b[..., 0] + b[..., 1]], g[2 * b[..., 2] + b[..., 3]]
+    g = torch.tensor([-7, -5, -1, -3, 7, 5, 1, 3], device=bits.device)
+    return g[4 * b[..., 0] + 2 * b[..., 1] + b[..., 2]], g[4 * b[..., 3] + 2 * b[..., 4] + b[..., 5]]
+
+
+def _signal_levels(mod, coding, length, device):
+    h = np.zeros(24, np.uint8)
+    code = RATE_NIBBLE[(mod, coding)]
+    h[0:4] = [(code >> k) & 1 for k in range(4)]
+    h[5:17] = [(length >> k) & 1 for k in range(12)]
+    h[17] ^= h.sum() & 1
+    coded = _encode(torch.from_numpy(h[None]).to(device), 0)[0]
+    il = torch.empty_like(coded)
+    il[torch.from_numpy(interleave_perm(0)).to(device)] = coded
+    re, _ = _map(il[:, None], 0)
+    return re * UNIT[0]
+
+
+def packets_freq(payloads, mod, coding, device="cpu"):
+    """Frequency-domain symbols (GetData order, TX units) for equal-length payloads.
+    payloads: uint8 numpy [n, L].  Returns int64 torch [n, 1 + nsym, 48, 2]."""
+    n, L = payloads.shape
+    nd, nc = ndbps(mod, coding), NCBPS[mod]
+    nsym = n_data_symbols(mod, coding, L)
+    nbits = nsym * nd
+    bits = np.zeros((n, nbits), np.uint8)
+    bits[:, 16:16 + 8 * L] = np.unpackbits(payloads, axis=1, bitorder="little")
+    crc = np.array([zlib.crc32(p.tobytes()) for p in payloads], np.uint32)
+    bits[:, 16 + 8 * L:16 + 8 * L + 32] = ((crc[:, None] >> np.arange(32, dtype=np.uint32)) & 1).astype(np.uint8)
+    bits ^= _scrambler_keystream(nbits)[None]
+    u = torch.from_numpy(bits).to(device)
+    coded = _encode(u, coding).reshape(n, nsym, nc)
+    perm = torch.from_numpy(interleave_perm(mod)).to(device)
+    il = torch.empty_like(coded)
+    il[:, :, perm] = coded
+    re, im = _map(il.reshape(n, nsym, 48, nc // 48), mod)
+    out = torch.zeros((n, 1 + nsym, 48, 2), dtype=torch.int64, device=device)
+    out[:, 1:, :, 0] = re * UNIT[mod]
+    out[:, 1:, :, 1] = im * UNIT[mod]
+    out[:, 0, :, 0] = _signal_levels(mod, coding, L + 4, device)
+    return out
+
+
+def to_time(freq, sigma, gen, atten=100.0):
+    """freq int64 [n, S, 48, 2] -> time-domain int16 [n, S, 64, 2] (Appendix E channel)."""
+    n, S = freq.shape[:2]
+    dev = freq.device
+    X = torch.zeros((n, S, 64), dtype=torch.complex64, device=dev)
+    bins = torch.tensor(DATA_BINS, device=dev)
+    X[:, :, bins] = torch.complex(freq[..., 0].float(), freq[..., 1].float()) / atten
+    pil = (torch.randint(0, 2, (n, S, 4), generator=gen, device=dev) * 2 - 1).float() * 107.0
+    X[:, :, torch.tensor(PILOT_BINS, device=dev)] = torch.complex(pil, torch.zeros_like(pil))
+    x = torch.fft.ifft(X, dim=-1) * 64.0
+    t = torch.stack([x.real, x.imag], -1)
+    if sigma > 0:
+        t = t + sigma * torch.randn(t.shape, generator=gen, device=dev)
+    return torch.clamp(torch.round(t), -32768, 32767).to(torch.int16)
+
+
+def make_batch(n, mod=3, coding=2, payload_len=1500, sigma=4.0, seed=0x5EED, device="cpu", chunk=2048):
+    """BASELINE config 3 shape by default: n packets of payload_len bytes at (mod, coding).
+    Returns dict(sym int16 [n*S,64,2], sym_off int64 [n], nsym int32 [n], payload uint8
+    [n, L], max_nsym)."""
+    rng = np.random.default_rng(seed)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    payloads = rng.integers(0, 256, (n, payload_len), dtype=np.uint8)
+    syms = []
+    for a in range(0, n, chunk):
+        f = packets_freq(payloads[a:a + chunk], mod, coding, device)
+        syms.append(to_time(f, sigma, gen).reshape(-1, 64, 2))
+    S = 1 + n_data_symbols(mod, coding, payload_len)
+    sym = torch.cat(syms, 0)
+    return dict(sym=sym, sym_off=torch.arange(n, dtype=torch.int64, device=device) * S,
+                nsym=torch.full((n,), S, dtype=torch.int32, device=device), payload=payloads,
+                max_nsym=S, mod=mod, coding=coding, payload_len=payload_len)
+
+
+MCS8 = [(0, 0), (0, 2), (1, 0), (1, 2), (2, 0), (2, 2), (3, 1), (3, 2)]
+
+
+def make_mixed(n, min_len=64, max_len=4095, sigma=4.0, seed=0x3C5, device="cpu"):
+    """BASELINE config 5: MCS uniform over the 8 rates, PSDU length (the PLCP LENGTH field,
+    payload + 4 CRC bytes) uniform in [min_len, max_len].  Lengths > 2048 are header errors
+    under the reference parser (parsePLCPHeader.blk:171-174) and decode to no payload."""
+    rng = np.random.default_rng(seed)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    mcs = rng.integers(0, 8, n)
+    lens = rng.integers(min_len, max_len + 1, n)
+    syms, offs, nsyms, pays, meta = [], [], [], [], []
+    off = 0
+    for i in range(n):
+        mod, cod = MCS8[int(mcs[i])]
+        L = int(lens[i]) - 4
+        pay = rng.integers(0, 256, (1, L), dtype=np.uint8)
+        f = packets_freq(pay, mod, cod, device)
+        t = to_time(f, sigma, gen).reshape(-1, 64, 2)
+        syms.append(t)
+        offs.append(off)
+        nsyms.append(t.shape[0])
+        off += t.shape[0]
+        pays.append(pay[0])
+        meta.append((mod, cod, L + 4))
+    return dict(sym=torch.cat(syms, 0), sym_off=torch.tensor(offs, dtype=torch.int64, device=device),
+                nsym=torch.tensor(nsyms, dtype=torch.int32, device=device), payload=pays,
+                meta=np.array(meta, np.int32), max_nsym=int(max(nsyms)))
