@@ -1,0 +1,66 @@
+"""Random cross-checks of the oracle against the reference bricks compiled from
+/root/reference (oracle/_ref).  Skipped where those bricks are not built (GPU box)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from tests.golden import synth
+
+
+@pytest.fixture(scope="module")
+def ref(oracle):
+    r = oracle.ref()
+    if r is None:
+        pytest.skip("reference bricks not built here (needs /root/reference)")
+    return r
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def test_fft_random(oracle, ref):
+    rng = np.random.default_rng(123)
+    for t in range(300):
+        x = rng.integers(-32768, 32768, (64, 2)).astype(np.int16)
+        o = np.zeros_like(x)
+        ref.zref_sora_fft(_p(o), 64, _p(x))
+        assert (oracle.fft64(x) == o).all()
+
+
+def test_viterbi_luts(oracle, ref):
+    ma = np.zeros(1024, np.uint8)
+    mb = np.zeros(1024, np.uint8)
+    ref.zref_viterbi_luts(_p(ma), _p(mb))
+    ma, mb = ma.reshape(64, 16), mb.reshape(64, 16)
+    for soft in range(8):
+        for k in range(8):
+            for j in range(16):
+                assert ma[soft * 8 + k, j] == oracle.vit_lut(0, soft, k, j)
+                assert mb[soft * 8 + k, j] == oracle.vit_lut(1, soft, k, j)
+
+
+def test_viterbi_random(oracle, ref):
+    rng = np.random.default_rng(9)
+    buf = np.zeros(12000, np.uint8)
+    for i in range(24):
+        cr, fl = int(rng.integers(0, 3)), int(rng.integers(1, 400))
+        s = synth.viterbi_soft(cr, fl, int(rng.integers(-1, 6)), seed=77 + i)
+        ref.zref_viterbi_init(fl, cr, 256)
+        outs = []
+        for k in range(0, s.size, 48):
+            c = np.ascontiguousarray(s[k:k + 48])
+            bits = ref.zref_viterbi_decode(_p(c), 48, _p(buf), 96000)
+            outs.append(buf[:bits // 8].copy())
+        assert (np.concatenate(outs) == oracle.viterbi_decode(s, fl, cr)).all()
+
+
+def test_shift_right(oracle, ref):
+    rng = np.random.default_rng(5)
+    for n in (1, 3, 4, 5, 9):
+        for sh in (0, 1, 15, 16, 20):
+            x = rng.integers(-32768, 32768, (n, 2)).astype(np.int16)
+            z = np.zeros_like(x)
+            ref.zref_v_shift_right_complex16(_p(z), _p(x), n, sh)
+            assert (z == oracle.v_shift_right_complex16(x, sh)).all()

@@ -29,6 +29,7 @@ using namespace zrx;
 
 struct zrx_ctx {
   int device = 0;
+  int vit_impl = 2;               // 2: k_viterbi2 (default); 1: k_viterbi (v1, A/B reference)
   hipStream_t stream = nullptr;
   bool timing = false;
   hipEvent_t ev[6] = {};
@@ -79,6 +80,14 @@ __global__ void k_fill_offsets(int64_t* off, int n, int64_t stride) {
 
 static inline int blocks(int64_t n, int per) { return (int)((n + per - 1) / per); }
 
+static void launch_viterbi(zrx_ctx* c, const uint8_t* soft, const int64_t* soft_off, const int32_t* params,
+                           int npkts, uint8_t* out, const int64_t* out_off, int32_t* out_bits) {
+  if (c->vit_impl == 1)
+    k_viterbi<<<blocks(npkts, 4), 256, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits, 256);
+  else
+    k_viterbi2<<<blocks(npkts, 4), 256, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits);
+}
+
 extern "C" {
 
 const char* zrx_version(void) { return "ziria_rx 0.1 (gfx950)"; }
@@ -92,6 +101,7 @@ int zrx_create(zrx_ctx** out, int device, void* stream) {
   zrx_ctx* c = new zrx_ctx();
   c->device = device;
   c->stream = (hipStream_t)stream;
+  if (const char* v = std::getenv("ZRX_VITERBI")) c->vit_impl = std::atoi(v) == 1 ? 1 : 2;
   for (auto& e : c->ev) ZRX_CHECK(hipEventCreate(&e));
   *out = c;
   return ZRX_OK;
@@ -163,8 +173,7 @@ int zrx_viterbi_dev(zrx_ctx* c, const int8_t* d_soft, const int64_t* d_soft_off,
                     int npkts, uint8_t* d_out, const int64_t* d_out_off, int32_t* d_out_bits) {
   if (!c || npkts < 0) return ZRX_EINVAL;
   if (npkts == 0) return ZRX_OK;
-  k_viterbi<<<blocks(npkts, 4), 256, 0, c->stream>>>((const uint8_t*)d_soft, d_soft_off, d_params, npkts, d_out,
-                                                       d_out_off, d_out_bits, 256);
+  launch_viterbi(c, (const uint8_t*)d_soft, d_soft_off, d_params, npkts, d_out, d_out_off, d_out_bits);
   ZRX_CHECK(hipGetLastError());
   return ZRX_OK;
 }
@@ -187,8 +196,7 @@ int zrx_rx_dev(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_sym_o
   k_data_fft<<<blocks(npkts, 4), 256, 0, s>>>((const uint4*)d_sym, d_sym_off, c->vparams, npkts, (uint4*)c->soft,
                                               c->soft_off);
   if (c->timing) ZRX_CHECK(hipEventRecord(c->ev[3], s));
-  k_viterbi<<<blocks(npkts, 4), 256, 0, s>>>(c->soft, c->soft_off, c->vparams, npkts, c->dec, c->dec_off,
-                                             c->dec_bits, 256);
+  launch_viterbi(c, c->soft, c->soft_off, c->vparams, npkts, c->dec, c->dec_off, c->dec_bits);
   if (c->timing) ZRX_CHECK(hipEventRecord(c->ev[4], s));
   k_descramble_crc<<<blocks(npkts, 4), 256, 0, s>>>(c->dec, c->dec_bits, d_info, d_payload, npkts);
   if (c->timing) ZRX_CHECK(hipEventRecord(c->ev[5], s));

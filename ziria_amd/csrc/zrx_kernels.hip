@@ -16,6 +16,7 @@
 #include <stdint.h>
 
 #include "zrx_device.hpp"
+#include "zrx_viterbi2.hpp"
 
 namespace zrx {
 

@@ -101,7 +101,7 @@ def viterbi_batch_decode(soft, pkt_soft_off, frame_len, code_rate, pkt_out_off=N
     cr = np.ascontiguousarray(code_rate, np.int16)
     n = so.size - 1
     if pkt_out_off is None:
-        pkt_out_off = np.concatenate([[0], np.cumsum(fl)[:-1]]).astype(np.int32)
+        pkt_out_off = (np.cumsum(fl) - fl).astype(np.int32)
     oo = np.ascontiguousarray(pkt_out_off, np.int32)
     total = int((oo + fl).max()) if n > 0 else 0
     out = np.zeros(max(total, 1), np.uint8)
