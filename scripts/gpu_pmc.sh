@@ -21,7 +21,7 @@ i=0
 for P in "$PMC1" "$PMC2" "$PMC3"; do
   [ -z "$P" ] && continue
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $P --output-format csv -d $R/gpurun_out/pmc$i -o pmc -- python3 $R/bench.py --npkts 4096 --steps 1 --warmup 0 --no-cpu > $R/gpurun_out/pmc$i.log 2>&1; rc=$?
+  timeout -k 10 300 rocprofv3 --pmc $P --output-format csv -d $R/gpurun_out/pmc$i -o pmc -- python3 $R/bench.py --npkts ${PMC_NPKTS:-4096} --steps 1 --warmup 0 --no-cpu > $R/gpurun_out/pmc$i.log 2>&1; rc=$?
   echo "pmc$i rc=$rc"; ok $rc || exit $rc
 done
 exit 0

@@ -11,14 +11,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(LIBDIR, "libziria_rx.so")
-SOURCES = ["zrx_api.hip", "zrx_kernels.hip", "zrx_device.hpp", "zrx_tables.h", "gen_tables.py"]
 
 
 def _stale():
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(HERE, "..", "include", "ziria_rx.h")]
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(HERE, "..", "include", "ziria_rx.h")]
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
