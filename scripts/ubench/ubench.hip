@@ -47,8 +47,6 @@
 #define I_READLANE(i) "v_readlane_b32 s0, %[r" #i "], 5\n\t"
 #define I_SWZ(i) "ds_swizzle_b32 %[r" #i "], %[r" #i "] offset:0x401F\n\t"
 #define I_BPERM(i) "ds_bpermute_b32 %[r" #i "], %[c], %[r" #i "]\n\t"
-#define I_SALU(i) "s_add_u32 s0, s0, %[s]\n\t"
-#define I_MIX(i) "v_add_u32 %[r" #i "], %[r" #i "], %[c]\n\ts_add_u32 s0, s0, %[s]\n\t"
 #define I_CMPU32(i) "v_cmp_eq_u32 vcc, %[r" #i "], %[c]\n\t"
 
 DEFK(k_add, I_ADD) DEFK(k_pkadd, I_PKADD) DEFK(k_pkmin, I_PKMIN) DEFK(k_pkaddsw, I_PKADDSW)
@@ -56,8 +54,7 @@ DEFK(k_xad, I_XAD) DEFK(k_sad, I_SAD) DEFK(k_andor, I_ANDOR) DEFK(k_align, I_ALI
 DEFK(k_adddpp, I_ADDDPP) DEFK(k_movdpp8, I_MOVDPP8) DEFK(k_mindpp, I_MINDPP) DEFK(k_cnddpp, I_CNDDPP)
 DEFK(k_addc, I_ADDC) DEFK(k_cmp16, I_CMP16) DEFK(k_cmp16sdwa, I_CMP16SDWA) DEFK(k_mul24, I_MUL24)
 DEFK(k_bfi, I_BFI) DEFK(k_perm, I_PERM) DEFK(k_pl32, I_PL32) DEFK(k_pl16, I_PL16)
-DEFK(k_readlane, I_READLANE) DEFK(k_swz, I_SWZ) DEFK(k_bperm, I_BPERM) DEFK(k_salu, I_SALU)
-DEFK(k_mix, I_MIX) DEFK(k_cmpu32, I_CMPU32)
+DEFK(k_readlane, I_READLANE) DEFK(k_swz, I_SWZ) DEFK(k_bperm, I_BPERM) DEFK(k_cmpu32, I_CMPU32)
 
 typedef void (*KF)(uint32_t*, uint32_t);
 int main() {
@@ -69,8 +66,8 @@ int main() {
       {"v_addc_co_u32", k_addc}, {"v_cmp_eq_u16", k_cmp16}, {"v_cmp_eq_u16_sdwa", k_cmp16sdwa},
       {"v_mul_u32_u24", k_mul24}, {"v_bfi_b32", k_bfi}, {"v_perm_b32", k_perm},
       {"v_permlane32_swap", k_pl32}, {"v_permlane16_swap", k_pl16}, {"v_readlane_b32", k_readlane},
-      {"ds_swizzle_b32", k_swz}, {"ds_bpermute_b32", k_bperm}, {"s_add_u32", k_salu},
-      {"v_add+s_add pair", k_mix}, {"v_cmp_eq_u32", k_cmpu32}};
+      {"ds_swizzle_b32", k_swz}, {"ds_bpermute_b32", k_bperm},
+      {"v_cmp_eq_u32", k_cmpu32}};
   hipDeviceProp_t p;
   hipGetDeviceProperties(&p, 0);
   const int cus = p.multiProcessorCount;
@@ -80,7 +77,7 @@ int main() {
   hipEventCreate(&a);
   hipEventCreate(&b);
   const double ghz = 2.4;
-  for (int wps : {1, 2, 4, 8}) {          // waves per SIMD
+  for (int wps : {2, 4, 8}) {          // waves per SIMD
     const int blocks = cus * wps;         // 256-thread block = 4 waves = one per SIMD
     for (auto& k : ks) {
       k.f<<<blocks, 256>>>(out, 7);
@@ -93,6 +90,7 @@ int main() {
       const double inst_per_simd = (double)wps * ITERS * 16;
       printf("wps=%d %-26s %7.3f ms  %6.2f cyc/wave-inst/SIMD (@%.1fGHz)\n", wps, k.n, ms,
              ms * 1e-3 * ghz * 1e9 / inst_per_simd, ghz);
+      fflush(stdout);
     }
   }
   return 0;

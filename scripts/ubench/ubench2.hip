@@ -94,7 +94,7 @@ int main() {
   hipEventCreate(&a);
   hipEventCreate(&b);
   const double ghz = 2.4;
-  for (int wps : {2, 8}) {          // waves per SIMD
+  for (int wps : {2, 4, 8}) {          // waves per SIMD
     const int blocks = cus * wps;         // 256-thread block = 4 waves = one per SIMD
     for (auto& k : ks) {
       k.f<<<blocks, 256>>>(out, 7);
