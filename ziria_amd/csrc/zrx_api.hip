@@ -29,7 +29,7 @@ using namespace zrx;
 
 struct zrx_ctx {
   int device = 0;
-  int vit_impl = 2;               // 2: k_viterbi2 (default); 1: k_viterbi (v1, A/B reference)
+  int vit_impl = 3;               // 3: k_viterbi3 (default); 2: k_viterbi2; 1: k_viterbi (A/B references)
   hipStream_t stream = nullptr;
   bool timing = false;
   hipEvent_t ev[6] = {};
@@ -84,6 +84,8 @@ static void launch_viterbi(zrx_ctx* c, const uint8_t* soft, const int64_t* soft_
                            int npkts, uint8_t* out, const int64_t* out_off, int32_t* out_bits) {
   if (c->vit_impl == 1)
     k_viterbi<<<blocks(npkts, 4), 256, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits, 256);
+  else if (c->vit_impl == 3)
+    k_viterbi3<<<blocks(npkts, v3::kRows), 256, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits);
   else
     k_viterbi2<<<blocks(npkts, 4), 256, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits);
 }
@@ -101,7 +103,10 @@ int zrx_create(zrx_ctx** out, int device, void* stream) {
   zrx_ctx* c = new zrx_ctx();
   c->device = device;
   c->stream = (hipStream_t)stream;
-  if (const char* v = std::getenv("ZRX_VITERBI")) c->vit_impl = std::atoi(v) == 1 ? 1 : 2;
+  if (const char* v = std::getenv("ZRX_VITERBI")) {
+    const int k = std::atoi(v);
+    c->vit_impl = (k >= 1 && k <= 3) ? k : 3;
+  }
   for (auto& e : c->ev) ZRX_CHECK(hipEventCreate(&e));
   *out = c;
   return ZRX_OK;

@@ -17,6 +17,7 @@
 
 #include "zrx_device.hpp"
 #include "zrx_viterbi2.hpp"
+#include "zrx_viterbi3.hpp"
 
 namespace zrx {
 

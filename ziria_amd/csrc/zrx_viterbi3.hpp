@@ -1,0 +1,364 @@
+// Batched Viterbi brick, v3: four packets per wave, 64 trellis positions per packet packed
+// as 16 lanes x 2 dwords x 2 16-bit halves.
+//
+// Same results as the brick driver loop (csrc/sora_ext_viterbi.cpp:66-153 over
+// csrc/viterbicore.hpp:105-239) bit for bit; tests/vit3_model.py restates this layout in
+// numpy and is checked against the oracle on the CPU.
+//
+//  * Labels rotate, positions stay: after t columns position p holds state rotl6(p, t mod 6),
+//    so one column maps every position's state j to rotl6(j) in place and the butterfly
+//    partner (state j ^ 32) sits at position p ^ (1 << (5 - t mod 6)).  Position bits 0/1 are
+//    the half/dword inside the lane (partners in registers); bits 2..5 are lane bits mapped
+//    to lane xor 1, 2, 15, 8 so each cross-lane partner is ONE DPP move inside the 16-lane
+//    row (quad_perm, quad_perm, row_mirror, row_ror:8).
+//  * Half = [H][pad]: H = the reference's u8 metric with its marker bit cleared (always
+//    even, wraps mod 256 in v_pk_add_u16), pad bit 7 = the marker = branch index of the
+//    source state, pad bits 6..0 = the previous decisions along the survivor path.  The
+//    candidates of one column always differ in the marker, so v_pk_min_u16 reproduces
+//    min_epu8 on (metric | marker) exactly and drags the path history along with the
+//    winner (register exchange at no extra cost).  The history is shifted by one bit per
+//    column (v_lshrrev + v_bfi), and every 8 columns the pads are stored to an LDS ring
+//    indexed by state: one byte there = 8 decoded bits, so the reference traceback
+//    (argmin of the signed (m<<8)|4s key, `lookahead` skipped columns, bytes from the end)
+//    becomes an argmin plus one dependent LDS read per output byte.
+//  * Branch metrics: a per-column pattern word P = [BM(A=0,B=0), BM(0,1), BM(1,0), BM(1,1)]
+//    (implicit depuncturing: A-only / B-only columns have their own P, :93-110) is built
+//    once per 24-column body by lanes 0..15 of each row and broadcast with ds_swizzle;
+//    each dword gets its own branch metric with one v_perm (per-lane selector) and its
+//    complement with one v_sub from a per-lane constant.
+#pragma once
+#include <utility>
+
+#include "zrx_device.hpp"
+
+namespace zrx {
+namespace v3 {
+
+constexpr int kRing = 39;                 // snapshot slots of 8 columns per packet (>= 38)
+constexpr int kRows = 16;                 // packets per 256-thread block
+constexpr int kSlotBytes = kRows * 64;
+constexpr uint32_t kNever = 0x7FFFFFFFu;
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 h2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__device__ __forceinline__ uint32_t w32(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+
+__host__ __device__ constexpr uint32_t rotl6(uint32_t x, uint32_t k) {
+  return k == 0 ? (x & 63u) : (((x << k) | (x >> (6u - k))) & 63u);
+}
+// position held by (lane-in-row l, dword d, half h): lane = b2*1 ^ b3*2 ^ b4*15 ^ b5*8
+__device__ __forceinline__ uint32_t pos_of(uint32_t l, uint32_t d, uint32_t h) {
+  const uint32_t b4 = (l >> 2) & 1u;
+  const uint32_t b2 = (l & 1u) ^ b4, b3 = ((l >> 1) & 1u) ^ b4, b5 = ((l >> 3) & 1u) ^ b4;
+  return h | (d << 1) | (b2 << 2) | (b3 << 3) | (b4 << 4) | (b5 << 5);
+}
+
+// Per-lane constants (registers for the whole kernel).
+struct Consts {
+  uint32_t sel[6][2];     // v_perm selector: [BM_hi][bm_hi<<7][BM_lo][bm_lo<<7]
+  uint32_t cf[6][2];      // per half (28 + bm) << 8: BY = cf - BX for a full column
+  uint32_t cs[6][2];      // per half (14 + bm) << 8: punctured column
+  uint32_t sa[3][4];      // LDS ring byte offset of the state held by position q at C mod 6 = 0,2,4
+};
+
+__device__ __forceinline__ void make_consts(Consts& K, uint32_t l, uint32_t rib) {
+#pragma unroll
+  for (int ph = 0; ph < 6; ph++) {
+#pragma unroll
+    for (int d = 0; d < 2; d++) {
+      uint32_t s = 0, cf = 0, cs = 0;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const uint32_t j = rotl6(pos_of(l, d, h), ph);
+        const uint32_t bm = (j >> 5) & 1u;
+        const uint32_t A = ((j >> 1) ^ (j >> 2) ^ (j >> 4)) & 1u;   // expected bits of j -> rotl6(j)
+        const uint32_t B = (j ^ (j >> 1) ^ (j >> 2)) & 1u;          // (encoding.blk:92-109)
+        s |= (bm ? 4u : 12u) << (16 * h);
+        s |= (2u * A + B) << (16 * h + 8);
+        cf |= (28u + bm) << (16 * h + 8);
+        cs |= (14u + bm) << (16 * h + 8);
+      }
+      K.sel[ph][d] = s; K.cf[ph][d] = cf; K.cs[ph][d] = cs;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 3; k++)
+#pragma unroll
+    for (int q = 0; q < 4; q++) K.sa[k][q] = rib * 64u + rotl6(pos_of(l, q >> 1, q & 1), 2 * k);
+}
+
+// One trellis column (phase PH = column index mod 6 before the step), KIND 0: (a, b) on
+// (A, B); 1: a on A only; 2: a on B only.
+template <int PH, int KIND>
+__device__ __forceinline__ void column(uint32_t& M0, uint32_t& M1, uint32_t P, const Consts& K) {
+  const uint32_t T0 = ((M0 >> 1) & 0x00FF00FFu) | (M0 & 0xFF00FF00u);
+  const uint32_t T1 = ((M1 >> 1) & 0x00FF00FFu) | (M1 & 0xFF00FF00u);
+  const uint32_t BX0 = __builtin_amdgcn_perm(0x80808080u, P, K.sel[PH][0]);
+  const uint32_t BX1 = __builtin_amdgcn_perm(0x80808080u, P, K.sel[PH][1]);
+  const uint32_t BY0 = (KIND == 0 ? K.cf[PH][0] : K.cs[PH][0]) - BX0;
+  const uint32_t BY1 = (KIND == 0 ? K.cf[PH][1] : K.cs[PH][1]) - BX1;
+  const u16x2 X0 = h2(T0) + h2(BX0), X1 = h2(T1) + h2(BX1);
+  const u16x2 Y0 = h2(T0) + h2(BY0), Y1 = h2(T1) + h2(BY1);
+  if constexpr (PH <= 3) {
+    constexpr int ctrl = PH == 0 ? 0x128 : PH == 1 ? 0x140 : PH == 2 ? 0x4E : 0xB1;  // xor 8, 15, 2, 1
+    const uint32_t Z0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)w32(Y0), ctrl, 0xF, 0xF, true);
+    const uint32_t Z1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)w32(Y1), ctrl, 0xF, 0xF, true);
+    M0 = w32(__builtin_elementwise_min(X0, h2(Z0)));
+    M1 = w32(__builtin_elementwise_min(X1, h2(Z1)));
+  } else if constexpr (PH == 4) {
+    M0 = w32(__builtin_elementwise_min(X0, Y1));
+    M1 = w32(__builtin_elementwise_min(X1, Y0));
+  } else {
+    M0 = w32(__builtin_elementwise_min(X0, Y0.yx));
+    M1 = w32(__builtin_elementwise_min(X1, Y1.yx));
+  }
+}
+
+// normalize (viterbicore.hpp:149-168): H -= min over the row's 64 H bytes (H even).
+__device__ __forceinline__ void normalize(uint32_t& M0, uint32_t& M1) {
+  const u16x2 t = __builtin_elementwise_min(h2(M0), h2(M1));
+  uint32_t v = (uint32_t)min(t.x, t.y);
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false));
+  const uint32_t rep = __builtin_amdgcn_perm(0u, v, 0x010C010Cu);   // [H][0][H][0]
+  M0 = w32(h2(M0) - h2(rep));
+  M1 = w32(h2(M1) - h2(rep));
+}
+
+// Rate tables: steps per group, soft values per group, soft values per 24-column body.
+template <int CR> struct Rate;
+template <> struct Rate<0> { static constexpr int steps = 1, G = 2, chunk = 48; };   // 1/2
+template <> struct Rate<1> { static constexpr int steps = 2, G = 3, chunk = 36; };   // 2/3
+template <> struct Rate<2> { static constexpr int steps = 3, G = 4, chunk = 32; };   // 3/4
+
+// Per-row decoder state (row-uniform values in VGPRs).
+struct Row {
+  uint32_t ob, end, cols, next;       // output bits so far, 8*frame_len+6, columns of input, next event column
+  bool live;                          // still decoding (not done, input not exhausted)
+  bool ppend, fpend;                  // partial / final traceback due at the body end
+  uint32_t pT, plook, fT, fcnt, flook;
+  uint32_t pM0, pM1, fM0, fM1;
+  uint32_t nbytes;                    // bytes written so far
+};
+
+__device__ __forceinline__ uint32_t row_next(const Row& R) {
+  if (!R.live) return kNever;
+  return min(min(R.ob + 286u, R.end), R.cols);
+}
+__device__ __forceinline__ uint32_t wave_min_rows(uint32_t v) {
+  const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 0), b = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+  const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)v, 32), d = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+  return min(min(a, b), min(c, d));
+}
+
+// Events after a group ending at column tr (sora_ext_viterbi.cpp:112-149); normalize ran first.
+__device__ __forceinline__ void events(Row& R, uint32_t tr, uint32_t M0, uint32_t M1) {
+  if (R.live && tr >= R.next) {
+    if (tr >= R.end) {                                  // final traceback
+      R.fpend = true; R.fM0 = M0; R.fM1 = M1; R.fT = tr;
+      R.fcnt = R.end - R.ob - 6u; R.flook = tr - R.end;
+      R.live = false;
+    } else if (tr >= R.ob + 286u) {                     // 256 bits, lookahead 24 + (tr-thresh)%8
+      R.ppend = true; R.pM0 = M0; R.pM1 = M1; R.pT = tr;
+      R.plook = 24u + ((tr - (R.ob + 286u)) & 7u);
+      R.ob += 256u;
+    }
+    if (tr >= R.cols) R.live = false;                   // input exhausted: no more groups
+    R.next = row_next(R);
+  }
+}
+
+// Traceback of one window for the rows with `due` set: argmin over the row (all lanes),
+// then one lane per row walks the snapshot ring and writes the window's bytes.
+__device__ __forceinline__ void traceback(bool due, uint32_t M0, uint32_t M1, uint32_t T, uint32_t cnt,
+                                          uint32_t look, uint32_t l, uint32_t rib, const uint8_t* ring,
+                                          uint8_t* __restrict__ out, uint32_t& nbytes) {
+  const uint32_t ph = T % 6u;
+  uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint32_t half = ((q >> 1) ? M1 : M0) >> (16 * (q & 1)) & 0xFFFFu;
+    const uint32_t st = rotl6(pos_of(l, q >> 1, q & 1), ph);
+    const uint32_t m = (half >> 8) | ((half >> 7) & 1u);
+    const uint32_t ukey = (((m << 8) | (st << 2)) & 0xFFFFu) ^ 0x8000u;   // signed int16 order
+    best = min(best, (ukey << 16) | (half & 0xFFu));
+  }
+  best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0xB1, 0xF, 0xF, false));
+  best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x4E, 0xF, 0xF, false));
+  best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x141, 0xF, 0xF, false));
+  best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x140, 0xF, 0xF, false));
+  if (!due || l != 0 || cnt == 0) return;
+  const uint32_t s0 = (best >> 18) & 63u, pad = best & 0xFFu;
+  const uint64_t Z = (uint64_t)s0 | ((uint64_t)(__builtin_bitreverse32(pad) >> 24) << 6);
+  const uint32_t C0 = T - ((T - 6u) & 7u);
+  uint32_t sc = (uint32_t)(Z >> (T - C0)) & 63u;
+  const uint32_t c_hi = T - look, c_first = c_hi + 8u - cnt;
+  uint32_t slot = ((C0 - 6u) >> 3) % (uint32_t)kRing;
+  const uint8_t* rb = ring + rib * 64u;
+  for (uint32_t C = C0; C >= c_first; C -= 8u) {
+    const uint32_t b = rb[slot * kSlotBytes + sc];
+    if (C <= c_hi) out[(C - 14u) >> 3] = (uint8_t)b;
+    sc = (__builtin_bitreverse32(b) >> 26) & 63u;
+    slot = slot == 0 ? (uint32_t)kRing - 1u : slot - 1u;
+  }
+  nbytes = max(nbytes, ((c_hi - 14u) >> 3) + 1u);
+}
+
+// P word of one column from its soft values (a, b) (BM(v, e) = e ? 14-2v : 2v, viterbilut.h)
+__device__ __forceinline__ uint32_t p_word(uint32_t r, uint32_t a, uint32_t b) {
+  const uint32_t a2 = (a & 7u) * 0x02020202u, b2 = (b & 7u) * 0x02020202u;
+  const uint32_t pa = a2 ^ 0x0E0E0000u, pb = a2 ^ 0x0E000E00u;
+  return r == 0 ? pa + (b2 ^ 0x0E000E00u) : (r == 1 ? pa : pb);
+}
+
+template <int CR>
+struct Packet {
+  using RT = Rate<CR>;
+  const Consts& K;
+  Row& R;
+  uint32_t l, rib;
+  uint8_t* ring;
+  uint8_t* __restrict__ out;
+
+  template <int J>
+  static __device__ __forceinline__ uint32_t bcast(uint32_t Pa, uint32_t Pb) {   // P word of body column J
+    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)(J < 16 ? Pa : Pb), ((J & 15) << 5) | 0x10);
+  }
+  template <int J, bool CHECKED>
+  __device__ __forceinline__ void col(uint32_t& M0, uint32_t& M1, uint32_t (&Pq)[4], uint32_t Pa, uint32_t Pb,
+                                      uint32_t tr0, uint32_t& s_next) {
+    const uint32_t P = Pq[J & 3];
+    if constexpr (J + 4 < 24) Pq[J & 3] = bcast<J + 4>(Pa, Pb);   // issued 4 columns ahead
+    constexpr int r = J % RT::steps;
+    column<J % 6, r>(M0, M1, P, K);
+    constexpr int c = J + 1;                           // column index within the body after the step
+    if constexpr (c % 8 == 6) {                        // snapshot column (C = 6 mod 8)
+      uint8_t* s = ring + (c >> 3) * kSlotBytes;
+      s[K.sa[c >> 3][0]] = (uint8_t)M0;
+      s[K.sa[c >> 3][1]] = (uint8_t)(M0 >> 16);
+      s[K.sa[c >> 3][2]] = (uint8_t)M1;
+      s[K.sa[c >> 3][3]] = (uint8_t)(M1 >> 16);
+    }
+    if constexpr (c % RT::steps == 0) {                // group end
+      if constexpr (c % 8 == 0 && (CR != 2 || c == 24)) normalize(M0, M1);
+      if constexpr (CHECKED) {
+        const uint32_t tr = tr0 + c;
+        if (tr >= s_next) {
+          events(R, tr, M0, M1);
+          s_next = wave_min_rows(R.next);
+        }
+      }
+    }
+  }
+  template <bool CHECKED, int... J>
+  __device__ __forceinline__ void body(uint32_t& M0, uint32_t& M1, uint32_t Pa, uint32_t Pb, uint32_t tr0,
+                                       uint32_t& s_next, std::integer_sequence<int, J...>) {
+    uint32_t Pq[4] = {bcast<0>(Pa, Pb), bcast<1>(Pa, Pb), bcast<2>(Pa, Pb), bcast<3>(Pa, Pb)};
+    (col<J, CHECKED>(M0, M1, Pq, Pa, Pb, tr0, s_next), ...);
+  }
+};
+
+// soft offset (within a body chunk) and kind of body column j
+template <int CR>
+__device__ __forceinline__ uint32_t soft_off(uint32_t j) {
+  constexpr uint32_t st = Rate<CR>::steps, G = Rate<CR>::G;
+  const uint32_t g = j / st, r = j % st;
+  return g * G + (r == 0 ? 0u : r + 1u);
+}
+
+template <int CR>
+__device__ void run_rows(const uint8_t* __restrict__ sp, uint32_t n, Row& R, const Consts& K, uint32_t l,
+                         uint32_t rib, uint8_t* ring_block, uint8_t* __restrict__ out) {
+  using RT = Rate<CR>;
+  const uint32_t p0 = pos_of(l, 0, 0), p1 = pos_of(l, 0, 1), p2 = pos_of(l, 1, 0), p3 = pos_of(l, 1, 1);
+  uint32_t M0 = ((p1 ? 48u : 0u) << 24) | ((p0 ? 48u : 0u) << 8);   // ALL_INIT0 (viterbilut.h:74-82)
+  uint32_t M1 = ((p3 ? 48u : 0u) << 24) | ((p2 ? 48u : 0u) << 8);
+  Packet<CR> pk{K, R, l, rib, ring_block, out};
+  // this lane builds the P words of body columns j1 = l and j2 = 16 + l (l < 8)
+  const uint32_t j1 = l, j2 = 16u + (l & 7u);
+  const uint32_t o1 = soft_off<CR>(j1), o2 = soft_off<CR>(j2);
+  const uint32_t r1 = j1 % RT::steps, r2 = j2 % RT::steps;
+  auto fetch = [&](uint32_t base, uint32_t o, uint32_t r, uint32_t& a, uint32_t& b) {
+    const uint32_t i = base + o;
+    a = i < n ? sp[i] : 0u;
+    b = (r == 0 && i + 1 < n) ? sp[i + 1] : 0u;
+  };
+  uint32_t a1, b1, a2, b2;
+  fetch(0, o1, r1, a1, b1);
+  fetch(0, o2, r2, a2, b2);
+  uint32_t s_next = wave_min_rows(R.next);
+  uint32_t slot = 0;                                   // first slot of this body (3 per body)
+  for (uint32_t tr0 = 0, base = 0; __builtin_amdgcn_ballot_w64(R.live) != 0; tr0 += 24, base += RT::chunk) {
+    const uint32_t Pa = p_word(r1, a1, b1), Pb = p_word(r2, a2, b2);
+    fetch(base + RT::chunk, o1, r1, a1, b1);           // next body's soft values (latency hidden)
+    fetch(base + RT::chunk, o2, r2, a2, b2);
+    pk.ring = ring_block + slot * kSlotBytes;
+    if (s_next > tr0 + 24)
+      pk.template body<false>(M0, M1, Pa, Pb, tr0, s_next, std::make_integer_sequence<int, 24>{});
+    else
+      pk.template body<true>(M0, M1, Pa, Pb, tr0, s_next, std::make_integer_sequence<int, 24>{});
+    slot = slot + 3 == kRing ? 0 : slot + 3;
+    if (__builtin_amdgcn_ballot_w64(R.ppend) != 0) {
+      traceback(R.ppend, R.pM0, R.pM1, R.pT, 256u, R.plook, l, rib, ring_block, out, R.nbytes);
+      R.ppend = false;
+    }
+    if (__builtin_amdgcn_ballot_w64(R.fpend) != 0) {
+      traceback(R.fpend, R.fM0, R.fM1, R.fT, R.fcnt, R.flook, l, rib, ring_block, out, R.nbytes);
+      R.fpend = false;
+    }
+  }
+}
+
+}  // namespace v3
+
+// vparams[4p..] = {frame_len, code_rate, soft_len, *}; out_bits[p] = bits written.
+// Requires depth 256 (the only depth the WiFi RX uses: Viterbi.blk:34).  Four packets per
+// wave (16 lanes each); rows of a wave may have different rates and lengths.
+__global__ __launch_bounds__(256, 4) void k_viterbi3(const uint8_t* __restrict__ soft, const int64_t* __restrict__ soft_off,
+                                                  const int32_t* __restrict__ vparams, int npkts,
+                                                  uint8_t* __restrict__ out, const int64_t* __restrict__ out_off,
+                                                  int32_t* __restrict__ out_bits) {
+  __shared__ uint8_t ring[v3::kRing * v3::kSlotBytes];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t l = lane & 15u;
+  const uint32_t rib = threadIdx.x >> 4;               // row (packet) in block
+  const int p = blockIdx.x * v3::kRows + (int)rib;
+  const bool valid = p < npkts;
+  int fl = 0, cr = 0, n = 0;
+  int64_t so = 0, oo = 0;
+  if (valid) {
+    const int32_t* vp = vparams + 4 * (int64_t)p;
+    fl = vp[0]; cr = vp[1]; n = vp[2];
+    so = soft_off[p]; oo = out_off[p];
+  }
+  v3::Row R;
+  R.ob = 0; R.end = (uint32_t)fl * 8u + 6u;
+  R.cols = valid && n > 0 && cr >= 0 && cr <= 2 ? (uint32_t)(n / (cr == 0 ? 2 : cr == 1 ? 3 : 4)) * (uint32_t)(cr + 1) : 0u;
+  R.live = R.cols > 0;
+  R.ppend = R.fpend = false;
+  R.pT = R.plook = R.fT = R.fcnt = R.flook = 0;
+  R.pM0 = R.pM1 = R.fM0 = R.fM1 = 0;
+  R.nbytes = 0;
+  R.next = v3::row_next(R);
+  v3::Consts K;
+  v3::make_consts(K, l, rib);
+  const uint8_t* sp = soft + so;
+  uint8_t* op = out + oo;
+  // rows of one rate run together; other rows of the wave sit out that pass
+  for (int rate = 0; rate < 3; rate++) {
+    const bool mine = R.live && cr == rate;
+    if (__builtin_amdgcn_ballot_w64(mine) == 0) continue;
+    v3::Row Rr = R;
+    Rr.live = mine;
+    Rr.next = v3::row_next(Rr);
+    if (rate == 0) v3::run_rows<0>(sp, (uint32_t)n, Rr, K, l, rib, ring, op);
+    else if (rate == 1) v3::run_rows<1>(sp, (uint32_t)n, Rr, K, l, rib, ring, op);
+    else v3::run_rows<2>(sp, (uint32_t)n, Rr, K, l, rib, ring, op);
+    if (mine) R.nbytes = Rr.nbytes;
+  }
+  if (valid && l == 0) out_bits[p] = (int32_t)(R.nbytes * 8u);
+}
+
+}  // namespace zrx
