@@ -6,7 +6,12 @@ synthetic time-domain packets already resident in HBM (BASELINE config 3: 16384 
 1500 B payload at 54 Mbps = 57 OFDM symbols each).  Multi-GPU: one process per GPU, each
 rank decodes its own 16384-packet batch (weak scaling, no collective in the hot loop);
 after the timed region the CRC-pass counts are all-reduced and the payload bytes gathered
-to rank 0 over RCCL.
+to rank 0 over RCCL (ziria_amd/node.py).
+
+Stage times come from HIP events recorded by the engine on its own stream around every
+kernel of every timed step (zrx_enable_timing), so `roofline.achieved` is measured live
+over the timed region.  `roofline.traffic` is the per-launch HBM byte count from the
+rocprofv3 PMC passes summarised in profiles/pmc_summary.json (scripts/pmc_summary.py).
 
 python bench.py [--gpus N --steps K --warmup W]   (N>1 under torch.distributed.run)
 """
@@ -16,19 +21,31 @@ import os
 import sys
 import time
 
-import numpy as np
 import torch
 import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from ziria_amd import txgen  # noqa: E402
+from ziria_amd import node, txgen  # noqa: E402
 from ziria_amd.engine import RxEngine  # noqa: E402
 
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz = 78.6
 HBM_PEAK_GBS = 8000.0
 OPS_PER_DECODED_BIT = 256                       # 64 ACS x (add, add, compare, select)
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
+
+
+def traffic_for(kernel, npkts):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (same workload)."""
+    try:
+        s = json.load(open(PMC_SUMMARY))
+        k = s["kernels"][kernel]
+        if int(s.get("npkts", -1)) != npkts:
+            return None
+        return k.get("hbm_bytes_per_launch")
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def main():
@@ -38,7 +55,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--npkts", type=int, default=16384)
     ap.add_argument("--payload", type=int, default=1500)
-    ap.add_argument("--cpu-sample", type=int, default=4096, help="packets in the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall time budget of the CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
@@ -71,45 +88,25 @@ def main():
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
+    eng.enable_timing(True)                       # stage events on the engine's stream, every step
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
-
-    # ---------------------------------------------------------------- bit-exact self-check
-    inf = info.cpu().numpy()
-    ok_local = int((inf[:, 4] == 1).sum())
-    match = bool((payload[:, :args.payload].cpu().numpy() == b["payload"]).all())
-    bits_local = int(((inf[:, 2] - 4) * 8 * (inf[:, 4] == 1)).sum())
-    cnt = torch.tensor([ok_local, bits_local, int(match)], dtype=torch.int64, device=dev)
-    gather_ms = 0.0
-    if world > 1:
-        dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
-        torch.cuda.synchronize()
-        tg = time.perf_counter()
-        pay = payload[:, :args.payload].contiguous()
-        gl = [torch.empty_like(pay) for _ in range(world)] if rank == 0 else None
-        dist.gather(pay, gl, dst=0)
-        torch.cuda.synchronize()
-        gather_ms = (time.perf_counter() - tg) * 1e3
-    ok_all, bits_all, match_all = (int(v) for v in cnt.tolist())
-
-    # ---------------------------------------------------------------- per-stage kernel timing
-    eng.enable_timing(True)
-    stage_sum = {}
-    nprof = max(3, min(args.steps, 10))
-    for _ in range(nprof):
-        step()
-        for k, v in eng.stage_ms().items():
-            stage_sum[k] = stage_sum.get(k, 0.0) + v
+    stage = eng.stage_ms()                        # averages over the K timed steps
     eng.enable_timing(False)
-    stage = {k: v / nprof for k, v in stage_sum.items()}
+    elapsed = node.max_over_ranks(t1 - t0, device=dev)
+
+    # ---------------------------------------------------------------- bit-exact self-check + gather
+    ok, bits, match = node.counts(info, payload=payload, expected=b["payload"])
+    torch.cuda.synchronize()
+    tg = time.perf_counter()
+    ok_all, bits_all, match_all, _ = node.combine(ok, bits, match, payload[:, :args.payload].contiguous(),
+                                                  device=dev)
+    torch.cuda.synchronize()
+    gather_ms = (time.perf_counter() - tg) * 1e3 if world > 1 else 0.0
 
     decoded_bits = n * (args.payload + 4 + 2) * 8          # Viterbi output bits per launch
     vit_ms = stage["data_viterbi"]
@@ -118,14 +115,13 @@ def main():
     fft_bytes = n * nsym_data * (256 + 288)                # complex16 symbol in + 64-QAM soft out
     fft_gbs = fft_bytes / (stage["data_fft_demap"] * 1e-3) / 1e9
 
-    payload_bits_per_step = bits_all                       # CRC-checked payload bits, all ranks
-    value = payload_bits_per_step * args.steps / elapsed / 1e6
+    value = bits_all * args.steps / elapsed / 1e6          # CRC-checked payload bits, all ranks
     ms_per_step = elapsed / args.steps * 1e3
 
     # ---------------------------------------------------------------- CPU baseline (rank 0, N=1)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(b, min(args.cpu_sample, n), args.payload)
+        cpu = cpu_baseline(b, args.payload, args.cpu_seconds)
 
     if rank == 0:
         line = {
@@ -148,14 +144,15 @@ def main():
                        "parallelism": f"packet-sharded x{world}"},
             "bit_exact_check": {"crc_pass": ok_all, "packets": n * world, "payload_match": match_all == world},
             "stage_ms": {k: round(v, 4) for k, v in stage.items()},
-            "roofline": {"kernel": "k_viterbi (data Viterbi)", "bound": "valu",
+            "roofline": {"kernel": "k_viterbi3 (data Viterbi)", "bound": "valu",
                          "achieved": round(achieved_tops, 3), "peak": round(VALU_PEAK_TOPS, 1),
                          "unit": "Tops/s", "frac": round(achieved_tops / VALU_PEAK_TOPS, 4),
-                         "traffic": None,
+                         "traffic": traffic_for("k_viterbi3", n),
                          "units": f"{OPS_PER_DECODED_BIT} int ops per decoded bit x {decoded_bits} bits/launch"},
             "roofline_fft": {"kernel": "k_data_fft (FFT64+GetData+demap+deinterleave)", "bound": "hbm",
                              "achieved": round(fft_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(fft_gbs / HBM_PEAK_GBS, 4),
+                             "traffic": traffic_for("k_data_fft", n),
                              "units": f"544 B per data symbol x {n * nsym_data} symbols/launch"},
             "gather_ms": round(gather_ms, 3),
             "cpu_baseline": cpu,
@@ -165,21 +162,28 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(b, sample, payload_len):
-    """The oracle (scalar C restatement, port) over a bounded sample of the same packets,
-    packet-parallel with pthreads over this process's host CPU share."""
+def cpu_baseline(b, payload_len, seconds):
+    """The oracle (scalar C restatement, "port") on the host cores this process may use,
+    packet-parallel with pthreads, over chunks of the same packets until `seconds` of wall
+    time have passed."""
     from oracle import oracle as O
-    threads = min(16, os.cpu_count() or 1)
+    threads = min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count() or 1)
     sym = b["sym"].cpu().numpy()
-    off = b["sym_off"][:sample].cpu().numpy()
-    ns = b["nsym"][:sample].cpu().numpy()
+    off_all = b["sym_off"].cpu().numpy()
+    ns_all = b["nsym"].cpu().numpy()
+    chunk = 1024
+    done = ok = 0
     t0 = time.perf_counter()
-    pay, res = O.rx_batch_time(sym, off, ns, nthreads=threads)
+    while time.perf_counter() - t0 < seconds:
+        lo = done % off_all.size
+        hi = min(lo + chunk, off_all.size)
+        _, res = O.rx_batch_time(sym, off_all[lo:hi], ns_all[lo:hi], nthreads=threads)
+        ok += sum(r["crc_ok"] for r in res)
+        done += hi - lo
     dt = time.perf_counter() - t0
-    ok = sum(r["crc_ok"] for r in res)
     bits = ok * payload_len * 8
     return {"value": round(bits / dt / 1e6, 2), "unit": "Mbit/s", "cores": threads, "kind": "port",
-            "sample": f"{sample} packets of the same batch ({ok} CRC-ok), {dt:.2f} s wall on {threads} threads"}
+            "sample": f"{done} packets of the same batch ({ok} CRC-ok), {dt:.1f} s wall on {threads} threads"}
 
 
 if __name__ == "__main__":

@@ -108,10 +108,13 @@ int zrx_set_stream(zrx_ctx* ctx, void* stream);
 /* Pre-allocates the workspace for rx batches of up to npkts packets whose largest
  * packet has max_nsym symbols (no allocation happens inside the launch functions). */
 int zrx_reserve(zrx_ctx* ctx, int npkts, int max_nsym);
-/* Per-stage HIP-event timing on the context's stream (0 = off). */
+/* Per-stage HIP-event timing on the context's stream (0 = off).  Turning it on (or off)
+ * starts a new measurement: every zrx_rx_dev launch from then on records its own events. */
 int zrx_enable_timing(zrx_ctx* ctx, int on);
-/* Stage durations (ms) of the last launch: [0] SIGNAL FFT+demap, [1] SIGNAL Viterbi+header,
- * [2] data FFT+demap+deinterleave, [3] data Viterbi, [4] descramble+CRC.  Synchronizes. */
+/* Average stage durations (ms) over the launches recorded since zrx_enable_timing or the
+ * previous zrx_get_timing: [0] SIGNAL FFT+demap, [1] SIGNAL Viterbi+header, [2] data
+ * FFT+demap+deinterleave, [3] data Viterbi, [4] descramble+CRC.  Synchronizes; all zero
+ * if nothing was recorded. */
 int zrx_get_timing(zrx_ctx* ctx, float* ms5);
 
 /* d_in/d_out: 64*nsym complex16 each (may alias). */

@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <array>
 #include <mutex>
 #include <vector>
 
@@ -32,7 +33,10 @@ struct zrx_ctx {
   int vit_impl = 3;               // 3: k_viterbi3 (default); 2: k_viterbi2; 1: k_viterbi (A/B references)
   hipStream_t stream = nullptr;
   bool timing = false;
-  hipEvent_t ev[6] = {};
+  // one set of 6 events per timed zrx_rx_dev launch since zrx_enable_timing (averaged by
+  // zrx_get_timing), so stages are timed live inside a run of back-to-back launches
+  std::vector<std::array<hipEvent_t, 6>> evsets;
+  size_t nrec = 0;
   // rx-chain workspace (zrx_reserve)
   int cap_pkts = 0, cap_nsym = 0;
   int64_t soft_stride = 0;
@@ -107,7 +111,6 @@ int zrx_create(zrx_ctx** out, int device, void* stream) {
     const int k = std::atoi(v);
     c->vit_impl = (k >= 1 && k <= 3) ? k : 3;
   }
-  for (auto& e : c->ev) ZRX_CHECK(hipEventCreate(&e));
   *out = c;
   return ZRX_OK;
 }
@@ -118,7 +121,8 @@ int zrx_destroy(zrx_ctx* c) {
   free_ws(c);
   (void)hipFree(c->vstream);
   (void)hipFree(c->small);
-  for (auto& e : c->ev) (void)hipEventDestroy(e);
+  for (auto& set : c->evsets)
+    for (auto& e : set) (void)hipEventDestroy(e);
   delete c;
   return ZRX_OK;
 }
@@ -132,13 +136,22 @@ int zrx_set_stream(zrx_ctx* c, void* stream) {
 int zrx_enable_timing(zrx_ctx* c, int on) {
   if (!c) return ZRX_EINVAL;
   c->timing = on != 0;
+  c->nrec = 0;
   return ZRX_OK;
 }
 
 int zrx_get_timing(zrx_ctx* c, float* ms5) {
   if (!c || !ms5) return ZRX_EINVAL;
-  ZRX_CHECK(hipEventSynchronize(c->ev[5]));
-  for (int i = 0; i < 5; i++) ZRX_CHECK(hipEventElapsedTime(&ms5[i], c->ev[i], c->ev[i + 1]));
+  for (int i = 0; i < 5; i++) ms5[i] = 0.f;
+  if (c->nrec == 0) return ZRX_OK;
+  ZRX_CHECK(hipEventSynchronize(c->evsets[c->nrec - 1][5]));
+  for (size_t k = 0; k < c->nrec; k++)
+    for (int i = 0; i < 5; i++) {
+      float ms = 0.f;
+      ZRX_CHECK(hipEventElapsedTime(&ms, c->evsets[k][i], c->evsets[k][i + 1]));
+      ms5[i] += ms / (float)c->nrec;
+    }
+  c->nrec = 0;
   return ZRX_OK;
 }
 
@@ -193,18 +206,27 @@ int zrx_rx_dev(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_sym_o
   }
   if (npkts == 0) return ZRX_OK;
   hipStream_t s = c->stream;
-  if (c->timing) ZRX_CHECK(hipEventRecord(c->ev[0], s));
+  hipEvent_t* ev = nullptr;
+  if (c->timing) {
+    if (c->nrec == c->evsets.size()) {
+      std::array<hipEvent_t, 6> set;
+      for (auto& e : set) ZRX_CHECK(hipEventCreate(&e));
+      c->evsets.push_back(set);
+    }
+    ev = c->evsets[c->nrec++].data();
+  }
+  if (ev) ZRX_CHECK(hipEventRecord(ev[0], s));
   k_signal_fft<<<blocks(npkts, 256), 256, 0, s>>>((const uint4*)d_sym, d_sym_off, d_nsym, npkts, (uint4*)c->sig_soft);
-  if (c->timing) ZRX_CHECK(hipEventRecord(c->ev[1], s));
+  if (ev) ZRX_CHECK(hipEventRecord(ev[1], s));
   k_signal_vit<<<blocks(npkts, 4), 256, 0, s>>>(c->sig_soft, d_nsym, npkts, c->vparams, d_info);
-  if (c->timing) ZRX_CHECK(hipEventRecord(c->ev[2], s));
+  if (ev) ZRX_CHECK(hipEventRecord(ev[2], s));
   k_data_fft<<<blocks(npkts, 4), 256, 0, s>>>((const uint4*)d_sym, d_sym_off, c->vparams, npkts, (uint4*)c->soft,
                                               c->soft_off);
-  if (c->timing) ZRX_CHECK(hipEventRecord(c->ev[3], s));
+  if (ev) ZRX_CHECK(hipEventRecord(ev[3], s));
   launch_viterbi(c, c->soft, c->soft_off, c->vparams, npkts, c->dec, c->dec_off, c->dec_bits);
-  if (c->timing) ZRX_CHECK(hipEventRecord(c->ev[4], s));
+  if (ev) ZRX_CHECK(hipEventRecord(ev[4], s));
   k_descramble_crc<<<blocks(npkts, 4), 256, 0, s>>>(c->dec, c->dec_bits, d_info, d_payload, npkts);
-  if (c->timing) ZRX_CHECK(hipEventRecord(c->ev[5], s));
+  if (ev) ZRX_CHECK(hipEventRecord(ev[5], s));
   ZRX_CHECK(hipGetLastError());
   return ZRX_OK;
 }
