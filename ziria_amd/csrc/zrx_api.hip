@@ -30,7 +30,8 @@ using namespace zrx;
 
 struct zrx_ctx {
   int device = 0;
-  int vit_impl = 3;               // 3: k_viterbi3 (default); 2: k_viterbi2; 1: k_viterbi (A/B references)
+  int v3dbg = 0;                  // ZRX_V3DBG: k_viterbi3 timing-experiment variants (wrong output)
+  int vit_impl = 3;              // 3: k_viterbi3 (default); 2: k_viterbi2; 1: k_viterbi (A/B references)
   hipStream_t stream = nullptr;
   bool timing = false;
   // one set of 6 events per timed zrx_rx_dev launch since zrx_enable_timing (averaged by
@@ -88,8 +89,15 @@ static void launch_viterbi(zrx_ctx* c, const uint8_t* soft, const int64_t* soft_
                            int npkts, uint8_t* out, const int64_t* out_off, int32_t* out_bits) {
   if (c->vit_impl == 1)
     k_viterbi<<<blocks(npkts, 4), 256, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits, 256);
-  else if (c->vit_impl == 3)
-    k_viterbi3<<<blocks(npkts, v3::kRows), 256, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits);
+  else if (c->vit_impl == 3) {
+    const dim3 g(blocks(npkts, v3::kRows)), b(256);
+    switch (c->v3dbg) {   // timing experiments only (ZRX_V3DBG); 0 is the product kernel
+#define ZRX_V3(D) case D: k_viterbi3<D><<<g, b, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits); break;
+      ZRX_V3(1) ZRX_V3(2) ZRX_V3(4) ZRX_V3(8) ZRX_V3(16) ZRX_V3(32) ZRX_V3(64)
+#undef ZRX_V3
+      default: k_viterbi3<0><<<g, b, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits);
+    }
+  }
   else
     k_viterbi2<<<blocks(npkts, 4), 256, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits);
 }
@@ -111,6 +119,7 @@ int zrx_create(zrx_ctx** out, int device, void* stream) {
     const int k = std::atoi(v);
     c->vit_impl = (k >= 1 && k <= 3) ? k : 3;
   }
+  if (const char* v = std::getenv("ZRX_V3DBG")) c->v3dbg = std::atoi(v);
   *out = c;
   return ZRX_OK;
 }
@@ -225,7 +234,7 @@ int zrx_rx_dev(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_sym_o
   if (ev) ZRX_CHECK(hipEventRecord(ev[3], s));
   launch_viterbi(c, c->soft, c->soft_off, c->vparams, npkts, c->dec, c->dec_off, c->dec_bits);
   if (ev) ZRX_CHECK(hipEventRecord(ev[4], s));
-  k_descramble_crc<<<blocks(npkts, 4), 256, 0, s>>>(c->dec, c->dec_bits, d_info, d_payload, npkts);
+  k_descramble_crc<<<blocks(npkts, kCrcWaves), 64 * kCrcWaves, 0, s>>>(c->dec, c->dec_bits, d_info, d_payload, npkts);
   if (ev) ZRX_CHECK(hipEventRecord(ev[5], s));
   ZRX_CHECK(hipGetLastError());
   return ZRX_OK;

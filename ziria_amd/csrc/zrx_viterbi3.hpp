@@ -171,10 +171,12 @@ __device__ __forceinline__ void events(Row& R, uint32_t tr, uint32_t M0, uint32_
 }
 
 // Traceback of one window for the rows with `due` set: argmin over the row (all lanes),
-// then one lane per row walks the snapshot ring and writes the window's bytes.
+// then one lane per row walks the snapshot ring and writes the window's bytes.  The walk is
+// a chain of dependent LDS reads (state -> byte -> state 8 columns back), so the loop body
+// keeps only the read, the bit reversal and the address add on that chain.
 __device__ __forceinline__ void traceback(bool due, uint32_t M0, uint32_t M1, uint32_t T, uint32_t cnt,
                                           uint32_t look, uint32_t l, uint32_t rib, const uint8_t* ring,
-                                          uint8_t* __restrict__ out, uint32_t& nbytes) {
+                                          uint8_t* __restrict__ out, uint32_t ooff, uint32_t& nbytes) {
   const uint32_t ph = T % 6u;
   uint32_t best = 0xFFFFFFFFu;
 #pragma unroll
@@ -191,17 +193,25 @@ __device__ __forceinline__ void traceback(bool due, uint32_t M0, uint32_t M1, ui
   best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x140, 0xF, 0xF, false));
   if (!due || l != 0 || cnt == 0) return;
   const uint32_t s0 = (best >> 18) & 63u, pad = best & 0xFFu;
-  const uint64_t Z = (uint64_t)s0 | ((uint64_t)(__builtin_bitreverse32(pad) >> 24) << 6);
-  const uint32_t C0 = T - ((T - 6u) & 7u);
-  uint32_t sc = (uint32_t)(Z >> (T - C0)) & 63u;
-  const uint32_t c_hi = T - look, c_first = c_hi + 8u - cnt;
-  uint32_t slot = ((C0 - 6u) >> 3) % (uint32_t)kRing;
-  const uint8_t* rb = ring + rib * 64u;
-  for (uint32_t C = C0; C >= c_first; C -= 8u) {
-    const uint32_t b = rb[slot * kSlotBytes + sc];
-    if (C <= c_hi) out[(C - 14u) >> 3] = (uint8_t)b;
-    sc = (__builtin_bitreverse32(b) >> 26) & 63u;
-    slot = slot == 0 ? (uint32_t)kRing - 1u : slot - 1u;
+  // bit i of Z = decision of column T + 6 - i along the best path (state bits, then the pad)
+  const uint32_t Z = s0 | ((__builtin_bitreverse32(pad) >> 24) << 6);
+  const uint32_t C0 = T - ((T - 6u) & 7u);             // newest snapshot column <= T
+  uint32_t sc = (Z >> (T - C0)) & 63u;
+  const uint32_t c_hi = T - look;
+  const uint32_t nlook = (C0 - c_hi) >> 3, nout = cnt >> 3;
+  const uint32_t lo = rib * 64u, wrap = (uint32_t)(kRing - 1) * kSlotBytes;
+  uint32_t a = lo + (((C0 - 6u) >> 3) % (uint32_t)kRing) * kSlotBytes;
+  for (uint32_t i = 0; i < nlook; i++) {               // lookahead blocks: state only
+    const uint32_t b = ring[a + sc];
+    sc = __builtin_bitreverse32(b) >> 26;
+    a = a >= lo + kSlotBytes ? a - kSlotBytes : a + wrap;
+  }
+  uint32_t o = ooff + ((c_hi - 14u) >> 3);             // output byte of block c_hi, newest first
+  for (uint32_t i = 0; i < nout; i++, o--) {
+    const uint32_t b = ring[a + sc];
+    out[o] = (uint8_t)b;
+    sc = __builtin_bitreverse32(b) >> 26;
+    a = a >= lo + kSlotBytes ? a - kSlotBytes : a + wrap;
   }
   nbytes = max(nbytes, ((c_hi - 14u) >> 3) + 1u);
 }
@@ -213,28 +223,42 @@ __device__ __forceinline__ uint32_t p_word(uint32_t r, uint32_t a, uint32_t b) {
   return r == 0 ? pa + (b2 ^ 0x0E000E00u) : (r == 1 ? pa : pb);
 }
 
-template <int CR>
+// DBG (timing experiments only, never selected by default): 1 skip the traceback walk,
+// 2 skip snapshot stores, 4 skip normalization, 8 no P broadcast, 16 never run checked bodies,
+// 32 broadcast P with DPP row_newbcast, 64 ds_swizzle issued 4 columns ahead behind a
+// scheduling barrier.
+template <int CR, int DBG = 0>
 struct Packet {
   using RT = Rate<CR>;
   const Consts& K;
   Row& R;
   uint32_t l, rib;
   uint8_t* ring;
-  uint8_t* __restrict__ out;
 
   template <int J>
   static __device__ __forceinline__ uint32_t bcast(uint32_t Pa, uint32_t Pb) {   // P word of body column J
-    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)(J < 16 ? Pa : Pb), ((J & 15) << 5) | 0x10);
+    if constexpr ((DBG & 32) != 0)
+      return (uint32_t)__builtin_amdgcn_mov_dpp((int)(J < 16 ? Pa : Pb), 0x150 + (J & 15), 0xF, 0xF, false);
+    else
+      return (uint32_t)__builtin_amdgcn_ds_swizzle((int)(J < 16 ? Pa : Pb), ((J & 15) << 5) | 0x10);
   }
   template <int J, bool CHECKED>
   __device__ __forceinline__ void col(uint32_t& M0, uint32_t& M1, uint32_t (&Pq)[4], uint32_t Pa, uint32_t Pb,
                                       uint32_t tr0, uint32_t& s_next) {
-    const uint32_t P = Pq[J & 3];
-    if constexpr (J + 4 < 24) Pq[J & 3] = bcast<J + 4>(Pa, Pb);   // issued 4 columns ahead
+    uint32_t P;
+    if constexpr ((DBG & 8) != 0) {
+      P = J < 16 ? Pa : Pb;
+    } else if constexpr ((DBG & 32) != 0) {
+      P = bcast<J>(Pa, Pb);
+    } else {
+      P = Pq[J & 3];
+      if constexpr (J + 4 < 24) Pq[J & 3] = bcast<J + 4>(Pa, Pb);   // issued 4 columns ahead
+      if constexpr ((DBG & 64) != 0) __builtin_amdgcn_sched_barrier(0);
+    }
     constexpr int r = J % RT::steps;
     column<J % 6, r>(M0, M1, P, K);
     constexpr int c = J + 1;                           // column index within the body after the step
-    if constexpr (c % 8 == 6) {                        // snapshot column (C = 6 mod 8)
+    if constexpr (c % 8 == 6 && !(DBG & 2)) {          // snapshot column (C = 6 mod 8)
       uint8_t* s = ring + (c >> 3) * kSlotBytes;
       s[K.sa[c >> 3][0]] = (uint8_t)M0;
       s[K.sa[c >> 3][1]] = (uint8_t)(M0 >> 16);
@@ -242,7 +266,7 @@ struct Packet {
       s[K.sa[c >> 3][3]] = (uint8_t)(M1 >> 16);
     }
     if constexpr (c % RT::steps == 0) {                // group end
-      if constexpr (c % 8 == 0 && (CR != 2 || c == 24)) normalize(M0, M1);
+      if constexpr (c % 8 == 0 && (CR != 2 || c == 24) && !(DBG & 4)) normalize(M0, M1);
       if constexpr (CHECKED) {
         const uint32_t tr = tr0 + c;
         if (tr >= s_next) {
@@ -255,7 +279,10 @@ struct Packet {
   template <bool CHECKED, int... J>
   __device__ __forceinline__ void body(uint32_t& M0, uint32_t& M1, uint32_t Pa, uint32_t Pb, uint32_t tr0,
                                        uint32_t& s_next, std::integer_sequence<int, J...>) {
-    uint32_t Pq[4] = {bcast<0>(Pa, Pb), bcast<1>(Pa, Pb), bcast<2>(Pa, Pb), bcast<3>(Pa, Pb)};
+    uint32_t Pq[4] = {0, 0, 0, 0};
+    if constexpr (!(DBG & 40)) {
+      Pq[0] = bcast<0>(Pa, Pb); Pq[1] = bcast<1>(Pa, Pb); Pq[2] = bcast<2>(Pa, Pb); Pq[3] = bcast<3>(Pa, Pb);
+    }
     (col<J, CHECKED>(M0, M1, Pq, Pa, Pb, tr0, s_next), ...);
   }
 };
@@ -268,14 +295,14 @@ __device__ __forceinline__ uint32_t soft_off(uint32_t j) {
   return g * G + (r == 0 ? 0u : r + 1u);
 }
 
-template <int CR>
+template <int CR, int DBG>
 __device__ void run_rows(const uint8_t* __restrict__ sp, uint32_t n, Row& R, const Consts& K, uint32_t l,
-                         uint32_t rib, uint8_t* ring_block, uint8_t* __restrict__ out) {
+                         uint32_t rib, uint8_t* ring_block, uint8_t* __restrict__ out, uint32_t ooff) {
   using RT = Rate<CR>;
   const uint32_t p0 = pos_of(l, 0, 0), p1 = pos_of(l, 0, 1), p2 = pos_of(l, 1, 0), p3 = pos_of(l, 1, 1);
   uint32_t M0 = ((p1 ? 48u : 0u) << 24) | ((p0 ? 48u : 0u) << 8);   // ALL_INIT0 (viterbilut.h:74-82)
   uint32_t M1 = ((p3 ? 48u : 0u) << 24) | ((p2 ? 48u : 0u) << 8);
-  Packet<CR> pk{K, R, l, rib, ring_block, out};
+  Packet<CR, DBG> pk{K, R, l, rib, ring_block};
   // this lane builds the P words of body columns j1 = l and j2 = 16 + l (l < 8)
   const uint32_t j1 = l, j2 = 16u + (l & 7u);
   const uint32_t o1 = soft_off<CR>(j1), o2 = soft_off<CR>(j2);
@@ -295,18 +322,22 @@ __device__ void run_rows(const uint8_t* __restrict__ sp, uint32_t n, Row& R, con
     fetch(base + RT::chunk, o1, r1, a1, b1);           // next body's soft values (latency hidden)
     fetch(base + RT::chunk, o2, r2, a2, b2);
     pk.ring = ring_block + slot * kSlotBytes;
-    if (s_next > tr0 + 24)
+    if ((DBG & 16) || s_next > tr0 + 24)
       pk.template body<false>(M0, M1, Pa, Pb, tr0, s_next, std::make_integer_sequence<int, 24>{});
     else
       pk.template body<true>(M0, M1, Pa, Pb, tr0, s_next, std::make_integer_sequence<int, 24>{});
     slot = slot + 3 == kRing ? 0 : slot + 3;
-    if (__builtin_amdgcn_ballot_w64(R.ppend) != 0) {
-      traceback(R.ppend, R.pM0, R.pM1, R.pT, 256u, R.plook, l, rib, ring_block, out, R.nbytes);
+    if ((DBG & 1) == 0 && __builtin_amdgcn_ballot_w64(R.ppend) != 0) {
+      traceback(R.ppend, R.pM0, R.pM1, R.pT, 256u, R.plook, l, rib, ring_block, out, ooff, R.nbytes);
       R.ppend = false;
     }
-    if (__builtin_amdgcn_ballot_w64(R.fpend) != 0) {
-      traceback(R.fpend, R.fM0, R.fM1, R.fT, R.fcnt, R.flook, l, rib, ring_block, out, R.nbytes);
+    if ((DBG & 1) == 0 && __builtin_amdgcn_ballot_w64(R.fpend) != 0) {
+      traceback(R.fpend, R.fM0, R.fM1, R.fT, R.fcnt, R.flook, l, rib, ring_block, out, ooff, R.nbytes);
       R.fpend = false;
+    }
+    if constexpr ((DBG & 1) != 0) R.ppend = R.fpend = false;
+    if constexpr ((DBG & 16) != 0) {                   // no events: stop at the input's end
+      if (tr0 + 24 >= R.cols) R.live = false;
     }
   }
 }
@@ -316,6 +347,7 @@ __device__ void run_rows(const uint8_t* __restrict__ sp, uint32_t n, Row& R, con
 // vparams[4p..] = {frame_len, code_rate, soft_len, *}; out_bits[p] = bits written.
 // Requires depth 256 (the only depth the WiFi RX uses: Viterbi.blk:34).  Four packets per
 // wave (16 lanes each); rows of a wave may have different rates and lengths.
+template <int DBG>
 __global__ __launch_bounds__(256, 4) void k_viterbi3(const uint8_t* __restrict__ soft, const int64_t* __restrict__ soft_off,
                                                   const int32_t* __restrict__ vparams, int npkts,
                                                   uint8_t* __restrict__ out, const int64_t* __restrict__ out_off,
@@ -345,7 +377,9 @@ __global__ __launch_bounds__(256, 4) void k_viterbi3(const uint8_t* __restrict__
   v3::Consts K;
   v3::make_consts(K, l, rib);
   const uint8_t* sp = soft + so;
-  uint8_t* op = out + oo;
+  // output bytes are addressed as out + 32-bit offset (one uniform base for the whole wave)
+  uint8_t* obase = out + (oo & ~(int64_t)0xFFFFFFFF);
+  const uint32_t ooff = (uint32_t)(oo & 0xFFFFFFFF);
   // rows of one rate run together; other rows of the wave sit out that pass
   for (int rate = 0; rate < 3; rate++) {
     const bool mine = R.live && cr == rate;
@@ -353,9 +387,9 @@ __global__ __launch_bounds__(256, 4) void k_viterbi3(const uint8_t* __restrict__
     v3::Row Rr = R;
     Rr.live = mine;
     Rr.next = v3::row_next(Rr);
-    if (rate == 0) v3::run_rows<0>(sp, (uint32_t)n, Rr, K, l, rib, ring, op);
-    else if (rate == 1) v3::run_rows<1>(sp, (uint32_t)n, Rr, K, l, rib, ring, op);
-    else v3::run_rows<2>(sp, (uint32_t)n, Rr, K, l, rib, ring, op);
+    if (rate == 0) v3::run_rows<0, DBG>(sp, (uint32_t)n, Rr, K, l, rib, ring, obase, ooff);
+    else if (rate == 1) v3::run_rows<1, DBG>(sp, (uint32_t)n, Rr, K, l, rib, ring, obase, ooff);
+    else v3::run_rows<2, DBG>(sp, (uint32_t)n, Rr, K, l, rib, ring, obase, ooff);
     if (mine) R.nbytes = Rr.nbytes;
   }
   if (valid && l == 0) out_bits[p] = (int32_t)(R.nbytes * 8u);
