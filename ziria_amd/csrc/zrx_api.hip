@@ -48,6 +48,8 @@ struct zrx_ctx {
   uint8_t* dec = nullptr;         // kDecStride B per packet
   int64_t* dec_off = nullptr;     // p * kDecStride
   int32_t* dec_bits = nullptr;
+  int32_t* order = nullptr;       // Viterbi packet order (k_vit_order)
+  bool use_order = true;          // ZRX_ORDER=0 turns the ordering off (A/B experiments)
   // per-call externals
   VitStream* vstream = nullptr;
   void* small = nullptr;          // staging for single calls
@@ -71,10 +73,10 @@ static int check_device(int device) {
 
 static void free_ws(zrx_ctx* c) {
   for (void* p : {(void*)c->sig_soft, (void*)c->vparams, (void*)c->soft, (void*)c->soft_off, (void*)c->dec,
-                  (void*)c->dec_off, (void*)c->dec_bits})
+                  (void*)c->dec_off, (void*)c->dec_bits, (void*)c->order})
     (void)hipFree(p);
   c->sig_soft = nullptr; c->vparams = nullptr; c->soft = nullptr; c->soft_off = nullptr;
-  c->dec = nullptr; c->dec_off = nullptr; c->dec_bits = nullptr;
+  c->dec = nullptr; c->dec_off = nullptr; c->dec_bits = nullptr; c->order = nullptr;
   c->cap_pkts = c->cap_nsym = 0;
 }
 
@@ -87,15 +89,22 @@ static inline int blocks(int64_t n, int per) { return (int)((n + per - 1) / per)
 
 static void launch_viterbi(zrx_ctx* c, const uint8_t* soft, const int64_t* soft_off, const int32_t* params,
                            int npkts, uint8_t* out, const int64_t* out_off, int32_t* out_bits) {
+  // rows of a k_viterbi3 wave should share a rate and length: order the batch first when the
+  // workspace has room for it (zrx_reserve); otherwise identity order (still exact)
+  const int32_t* order = nullptr;
+  if (c->vit_impl == 3 && c->use_order && c->order && npkts <= c->cap_pkts && npkts <= kOrderMax) {
+    k_vit_order<<<1, 1024, 0, c->stream>>>(params, npkts, c->order);
+    order = c->order;
+  }
   if (c->vit_impl == 1)
     k_viterbi<<<blocks(npkts, 4), 256, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits, 256);
   else if (c->vit_impl == 3) {
     const dim3 g(blocks(npkts, v3::kRows)), b(256);
     switch (c->v3dbg) {   // timing experiments only (ZRX_V3DBG); 0 is the product kernel
-#define ZRX_V3(D) case D: k_viterbi3<D><<<g, b, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits); break;
+#define ZRX_V3(D) case D: k_viterbi3<D><<<g, b, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits, order); break;
       ZRX_V3(1) ZRX_V3(2) ZRX_V3(4) ZRX_V3(8) ZRX_V3(16) ZRX_V3(32) ZRX_V3(64)
 #undef ZRX_V3
-      default: k_viterbi3<0><<<g, b, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits);
+      default: k_viterbi3<0><<<g, b, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits, order);
     }
   }
   else
@@ -120,6 +129,7 @@ int zrx_create(zrx_ctx** out, int device, void* stream) {
     c->vit_impl = (k >= 1 && k <= 3) ? k : 3;
   }
   if (const char* v = std::getenv("ZRX_V3DBG")) c->v3dbg = std::atoi(v);
+  if (const char* v = std::getenv("ZRX_ORDER")) c->use_order = std::atoi(v) != 0;
   *out = c;
   return ZRX_OK;
 }
@@ -178,6 +188,7 @@ int zrx_reserve(zrx_ctx* c, int npkts, int max_nsym) {
   ZRX_CHECK(hipMalloc(&c->dec, (size_t)np * kDecStride + 256));
   ZRX_CHECK(hipMalloc(&c->dec_off, (size_t)np * 8 + 8));
   ZRX_CHECK(hipMalloc(&c->dec_bits, (size_t)np * 4 + 4));
+  ZRX_CHECK(hipMalloc(&c->order, (size_t)np * 4 + 4));
   if (np > 0) {
     k_fill_offsets<<<blocks(np, 256), 256, 0, c->stream>>>(c->soft_off, np, stride);
     k_fill_offsets<<<blocks(np, 256), 256, 0, c->stream>>>(c->dec_off, np, kDecStride);
@@ -414,6 +425,8 @@ int32_t __ext_viterbi_batch_decode(int8_t* soft, int softlen, int32_t* pkt_soft_
   }
   std::lock_guard<std::mutex> lk(g_mu);
   zrx_ctx* c = default_ctx();
+  int rc0 = zrx_reserve(c, np, 1);                   // room for the packet order of k_vit_order
+  if (rc0) return rc0;
   const size_t s_soft = ((size_t)softlen + 255) / 256 * 256, s_par = (size_t)np * 16, s_off = (size_t)np * 8;
   const size_t s_out = ((size_t)out_bytes + 255) / 256 * 256;
   uint8_t* d = (uint8_t*)staging(c, s_soft + s_par + 2 * s_off + s_out + (size_t)np * 4 + 1024);

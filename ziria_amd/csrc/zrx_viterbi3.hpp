@@ -346,18 +346,21 @@ __device__ void run_rows(const uint8_t* __restrict__ sp, uint32_t n, Row& R, con
 
 // vparams[4p..] = {frame_len, code_rate, soft_len, *}; out_bits[p] = bits written.
 // Requires depth 256 (the only depth the WiFi RX uses: Viterbi.blk:34).  Four packets per
-// wave (16 lanes each); rows of a wave may have different rates and lengths.
+// wave (16 lanes each); rows of a wave may have different rates and lengths (a wave runs one
+// pass per rate present), so mixed batches are first ordered by k_vit_order.  order may be
+// null (identity).
 template <int DBG>
 __global__ __launch_bounds__(256, 4) void k_viterbi3(const uint8_t* __restrict__ soft, const int64_t* __restrict__ soft_off,
                                                   const int32_t* __restrict__ vparams, int npkts,
                                                   uint8_t* __restrict__ out, const int64_t* __restrict__ out_off,
-                                                  int32_t* __restrict__ out_bits) {
+                                                  int32_t* __restrict__ out_bits, const int32_t* __restrict__ order) {
   __shared__ uint8_t ring[v3::kRing * v3::kSlotBytes];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t l = lane & 15u;
   const uint32_t rib = threadIdx.x >> 4;               // row (packet) in block
-  const int p = blockIdx.x * v3::kRows + (int)rib;
-  const bool valid = p < npkts;
+  const int slot_p = blockIdx.x * v3::kRows + (int)rib;   // row slot; order[] maps it to a packet
+  const bool valid = slot_p < npkts;
+  const int p = valid && order ? order[slot_p] : slot_p;
   int fl = 0, cr = 0, n = 0;
   int64_t so = 0, oo = 0;
   if (valid) {
@@ -393,6 +396,74 @@ __global__ __launch_bounds__(256, 4) void k_viterbi3(const uint8_t* __restrict__
     if (mine) R.nbytes = Rr.nbytes;
   }
   if (valid && l == 0) out_bits[p] = (int32_t)(R.nbytes * 8u);
+}
+
+// Packet order for k_viterbi3 over a mixed batch (BASELINE config 5): by code rate, then by
+// trellis length, longest first, so the four rows of a wave share one rate and similar
+// lengths.  One 1024-thread block; counting sort over (rate, 24-column bodies) keys, with
+// runs of equal keys in a thread's contiguous slice counted by one LDS atomic (a uniform
+// batch costs 1024 atomics, not one per packet).
+constexpr int kOrderLen = 512;                         // length buckets of 24 columns
+constexpr int kOrderKeys = 3 * kOrderLen + 1;          // + one bucket for packets with no work
+__device__ __forceinline__ uint32_t order_key(const int32_t* __restrict__ vparams, int p) {
+  const int32_t* vp = vparams + 4 * (int64_t)p;
+  const int cr = vp[1], n = vp[2];
+  if (n <= 0 || cr < 0 || cr > 2) return 3u * kOrderLen;
+  const uint32_t cols = (uint32_t)(n / (cr == 0 ? 2 : cr == 1 ? 3 : 4)) * (uint32_t)(cr + 1);
+  const uint32_t bodies = min((cols + 23u) / 24u, (uint32_t)kOrderLen - 1u);
+  return (uint32_t)cr * kOrderLen + (kOrderLen - 1u - bodies);
+}
+constexpr int kOrderMax = 32768;                       // batch size the LDS key stage holds
+__global__ __launch_bounds__(1024) void k_vit_order(const int32_t* __restrict__ vparams, int npkts,
+                                                    int32_t* __restrict__ order) {
+  __shared__ uint32_t hist[kOrderKeys];
+  __shared__ uint16_t keys[kOrderMax];
+  for (int i = threadIdx.x; i < kOrderKeys; i += blockDim.x) hist[i] = 0;
+  for (int p = threadIdx.x; p < npkts; p += blockDim.x) keys[p] = (uint16_t)order_key(vparams, p);  // coalesced
+  __syncthreads();
+  const int per = (npkts + (int)blockDim.x - 1) / (int)blockDim.x;
+  const int lo = min((int)threadIdx.x * per, npkts), hi = min(lo + per, npkts);
+  uint32_t prev = 0xFFFFFFFFu, run = 0;
+  for (int p = lo; p < hi; p++) {
+    const uint32_t k = keys[p];
+    if (k == prev) { run++; continue; }
+    if (run) atomicAdd(&hist[prev], run);
+    prev = k; run = 1;
+  }
+  if (run) atomicAdd(&hist[prev], run);
+  __syncthreads();
+  {                                                    // exclusive scan: 2 buckets per thread
+    __shared__ uint32_t wsum[16];
+    const int t = threadIdx.x, i0 = 2 * t, i1 = 2 * t + 1;
+    const uint32_t v0 = i0 < kOrderKeys ? hist[i0] : 0u, v1 = i1 < kOrderKeys ? hist[i1] : 0u;
+    const uint32_t mine = v0 + v1;
+    uint32_t inc = mine;                               // inclusive scan inside the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = (uint32_t)__shfl_up((int)inc, o);
+      if ((t & 63) >= o) inc += u;
+    }
+    if ((t & 63) == 63) wsum[t >> 6] = inc;
+    __syncthreads();
+    uint32_t wbase = 0;
+    for (int w = 0; w < (t >> 6); w++) wbase += wsum[w];
+    const uint32_t ex = wbase + inc - mine;
+    __syncthreads();
+    if (i0 < kOrderKeys) hist[i0] = ex;
+    if (i1 < kOrderKeys) hist[i1] = ex + v0;
+  }
+  __syncthreads();
+  prev = 0xFFFFFFFFu; run = 0;
+  int start = lo;
+  for (int p = lo; p <= hi; p++) {
+    const uint32_t k = p < hi ? (uint32_t)keys[p] : 0xFFFFFFFEu;
+    if (k == prev) { run++; continue; }
+    if (run) {
+      const uint32_t base = atomicAdd(&hist[prev], run);
+      for (uint32_t j = 0; j < run; j++) order[base + j] = start + (int)j;
+    }
+    prev = k; run = 1; start = p;
+  }
 }
 
 }  // namespace zrx
