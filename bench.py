@@ -14,6 +14,11 @@ over the timed region.  `roofline.traffic` is the per-launch HBM byte count from
 rocprofv3 PMC passes summarised in profiles/pmc_summary.json (scripts/pmc_summary.py).
 
 python bench.py [--gpus N --steps K --warmup W]   (N>1 under torch.distributed.run)
+
+Secondary workloads (our own reporting, not the driver's line): --config 2 = BASELINE
+config 2, the batched Viterbi alone (4096 x 1500-byte frames, rate 1/2, soft input in HBM);
+--config 5 = BASELINE config 5, mixed MCS (8 rates, PSDU length 64..4095 B; lengths above
+2048 are header errors under the reference parser and carry no payload).
 """
 import argparse
 import json
@@ -21,6 +26,7 @@ import os
 import sys
 import time
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -57,7 +63,12 @@ def main():
     ap.add_argument("--payload", type=int, default=1500)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall time budget of the CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 5])
     args = ap.parse_args()
+    if args.config == 2:
+        return bench_viterbi_only(args)
+    if args.config == 5:
+        return bench_mixed(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -160,6 +171,112 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _timed(step, steps, warmup):
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
+def bench_viterbi_only(args):
+    """BASELINE config 2: 4096 frames of 1500 bytes, rate 1/2, soft = 7*bit + U[-2,2] clipped
+    to [0,7], 24048 soft values per frame (48-value groups), all resident in HBM."""
+    from oracle import oracle as O
+    dev = torch.device("cuda", 0)
+    n = args.npkts if args.npkts != 16384 else 4096
+    fl = args.payload
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(0x5EED)
+    nbits = 8 * fl + 6
+    L = -(-nbits // 24) * 24                                  # 24 input bits per 48 soft values
+    u = torch.zeros((n, L), dtype=torch.uint8, device=dev)
+    u[:, :8 * fl] = torch.randint(0, 2, (n, 8 * fl), generator=gen, device=dev, dtype=torch.uint8)
+    coded = txgen._encode(u, 0).to(torch.int16)
+    noise = torch.randint(-2, 3, coded.shape, generator=gen, device=dev, dtype=torch.int16)
+    soft = torch.clamp(coded * 7 + noise, 0, 7).to(torch.int8).contiguous()
+    ns = soft.shape[1]
+    soft = soft.reshape(-1)
+    soft_off = torch.arange(n, dtype=torch.int64, device=dev) * ns
+    params = torch.tensor([fl, 0, ns, 0], dtype=torch.int32, device=dev).repeat(n, 1).contiguous()
+    stride = -(-fl // 16) * 16
+    out = torch.zeros(n * stride, dtype=torch.uint8, device=dev)
+    out_off = torch.arange(n, dtype=torch.int64, device=dev) * stride
+    out_bits = torch.zeros(n, dtype=torch.int32, device=dev)
+    eng = RxEngine(0)
+    eng.reserve(n, 1)
+    step = lambda: eng.viterbi(soft, soft_off, params, out, out_off, out_bits)
+    elapsed = _timed(step, args.steps, args.warmup)
+    sent = torch.from_numpy(np.packbits(u[:, :8 * fl].cpu().numpy(), axis=1, bitorder="little"))
+    got = out.reshape(n, stride)[:, :fl].cpu()
+    match = bool((got == sent).all()) and bool((out_bits == 8 * fl).all())
+    bits = n * fl * 8
+    # oracle on a bounded sample, single thread (informational)
+    sample = min(64, n)
+    s_np = soft[: sample * ns].cpu().numpy()
+    t0 = time.perf_counter()
+    for i in range(sample):
+        O.viterbi_decode(s_np[i * ns:(i + 1) * ns], fl, 0)
+    cpu_dt = time.perf_counter() - t0
+    print(json.dumps({
+        "metric": "decoded Mbit/s, batched K=7 rate-1/2 Viterbi only (BASELINE config 2)",
+        "value": round(bits * args.steps / elapsed / 1e6, 1), "unit": "Mbit/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (random bits, 802.11a encoder, soft 7*bit+U[-2,2])",
+        "config": {"workload": f"config2: {n} frames x {fl} B, R=1/2, {ns} soft values each"},
+        "bit_exact_check": {"frames_equal_sent": match},
+        "cpu_baseline": {"value": round(sample * fl * 8 / cpu_dt / 1e6, 2), "unit": "Mbit/s", "cores": 1,
+                         "kind": "port", "sample": f"{sample} frames, oracle brick loop, {cpu_dt:.2f} s"},
+    }), flush=True)
+
+
+def bench_mixed(args):
+    """BASELINE config 5: mixed MCS batch through the whole chain."""
+    from oracle import oracle as O
+    dev = torch.device("cuda", 0)
+    n = args.npkts if args.npkts != 16384 else 2048
+    m = txgen.make_mixed(n, min_len=64, max_len=4095, sigma=3.0, seed=0x3C5, device=dev)
+    S = m["max_nsym"]
+    eng = RxEngine(0)
+    eng.reserve(n, S)
+    payload = torch.zeros((n, 4096), dtype=torch.uint8, device=dev)
+    info = torch.zeros((n, 8), dtype=torch.int32, device=dev)
+    step = lambda: eng.rx(m["sym"], m["sym_off"], m["nsym"], S, payload, info)
+    eng.enable_timing(True)
+    elapsed = _timed(step, args.steps, args.warmup)
+    stage = eng.stage_ms()
+    eng.enable_timing(False)
+    inf = info.cpu().numpy()
+    pay = payload.cpu().numpy()
+    ok = inf[:, 4] == 1
+    good = all((pay[i, :len(m["payload"][i])] == m["payload"][i]).all() for i in range(n) if ok[i])
+    expect_ok = int((m["meta"][:, 2] <= 2048).sum())
+    bits = int(((inf[:, 2] - 4) * 8 * ok).sum())
+    sample = min(256, n)
+    t0 = time.perf_counter()
+    _, res = O.rx_batch_time(m["sym"].cpu().numpy(), m["sym_off"][:sample].cpu().numpy(),
+                             m["nsym"][:sample].cpu().numpy(), nthreads=min(16, os.cpu_count() or 1))
+    cpu_dt = time.perf_counter() - t0
+    cpu_bits = sum((r["len"] - 4) * 8 for r in res if r["crc_ok"])
+    print(json.dumps({
+        "metric": "decoded Mbit/s, mixed-MCS 802.11a RX chain (BASELINE config 5)",
+        "value": round(bits * args.steps / elapsed / 1e6, 1), "unit": "Mbit/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int16+u8",
+        "data": "synthetic (txgen.make_mixed: 8 MCS, PSDU 64..4095 B, AWGN sigma=3)",
+        "config": {"workload": f"config5: {n} packets, {S} symbols max"},
+        "bit_exact_check": {"crc_pass": int(ok.sum()), "expected_crc_pass": expect_ok, "payload_match": good},
+        "stage_ms": {k: round(v, 4) for k, v in stage.items()},
+        "cpu_baseline": {"value": round(cpu_bits / cpu_dt / 1e6, 2), "unit": "Mbit/s",
+                         "cores": min(16, os.cpu_count() or 1), "kind": "port",
+                         "sample": f"first {sample} packets, {cpu_dt:.2f} s"},
+    }), flush=True)
 
 
 def cpu_baseline(b, payload_len, seconds):
