@@ -8,6 +8,10 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_lib", "libziria_rx.so")
+# A/B timing experiments only: ZRX_LIB_VARIANT=name loads _lib/libziria_rx.<name>.so, an
+# engine built from another revision by scripts/build_variant.sh.
+if os.environ.get("ZRX_LIB_VARIANT"):
+    LIB_PATH = os.path.join(HERE, "_lib", "libziria_rx.%s.so" % os.environ["ZRX_LIB_VARIANT"])
 
 _lib = None
 

@@ -46,6 +46,11 @@ __device__ __forceinline__ uint32_t w32(u16x2 x) { return __builtin_bit_cast(uin
 __host__ __device__ constexpr uint32_t rotl6(uint32_t x, uint32_t k) {
   return k == 0 ? (x & 63u) : (((x << k) | (x >> (6u - k))) & 63u);
 }
+// 6-bit reversal: the snapshot ring is indexed by rev6(state), so the walk's next index is
+// the low 6 bits of the byte it just read (next state = rev6(byte & 63)).
+__host__ __device__ constexpr uint32_t rev6(uint32_t x) {
+  return ((x & 1u) << 5) | ((x & 2u) << 3) | ((x & 4u) << 1) | ((x & 8u) >> 1) | ((x & 16u) >> 3) | ((x & 32u) >> 5);
+}
 // position held by (lane-in-row l, dword d, half h): lane = b2*1 ^ b3*2 ^ b4*15 ^ b5*8
 __device__ __forceinline__ uint32_t pos_of(uint32_t l, uint32_t d, uint32_t h) {
   const uint32_t b4 = (l >> 2) & 1u;
@@ -84,7 +89,7 @@ __device__ __forceinline__ void make_consts(Consts& K, uint32_t l, uint32_t rib)
 #pragma unroll
   for (int k = 0; k < 3; k++)
 #pragma unroll
-    for (int q = 0; q < 4; q++) K.sa[k][q] = rib * 64u + rotl6(pos_of(l, q >> 1, q & 1), 2 * k);
+    for (int q = 0; q < 4; q++) K.sa[k][q] = rib * 64u + rev6(rotl6(pos_of(l, q >> 1, q & 1), 2 * k));
 }
 
 // One trellis column (phase PH = column index mod 6 before the step), KIND 0: (a, b) on
@@ -196,29 +201,31 @@ __device__ __forceinline__ void traceback(bool due, uint32_t M0, uint32_t M1, ui
   // bit i of Z = decision of column T + 6 - i along the best path (state bits, then the pad)
   const uint32_t Z = s0 | ((__builtin_bitreverse32(pad) >> 24) << 6);
   const uint32_t C0 = T - ((T - 6u) & 7u);             // newest snapshot column <= T
-  uint32_t sc = (Z >> (T - C0)) & 63u;
+  uint32_t ix = __builtin_bitreverse32((Z >> (T - C0)) & 63u) >> 26;   // ring index = rev6(state)
   const uint32_t c_hi = T - look;
   const uint32_t nlook = (C0 - c_hi) >> 3, nout = cnt >> 3;
-  const uint32_t lo = rib * 64u, wrap = (uint32_t)(kRing - 1) * kSlotBytes;
-  uint32_t a = lo + (((C0 - 6u) >> 3) % (uint32_t)kRing) * kSlotBytes;
+  constexpr uint32_t span = (uint32_t)kRing * kSlotBytes;
+  // previous slot: x - 1024, wrapping below slot 0 by one unsigned min (no compare + select)
+  auto prev = [](uint32_t x) { const uint32_t y = x - (uint32_t)kSlotBytes; return min(y, y + span); };
+  uint32_t a = rib * 64u + (((C0 - 6u) >> 3) % (uint32_t)kRing) * kSlotBytes;
   for (uint32_t i = 0; i < nlook; i++) {               // lookahead blocks: state only
-    const uint32_t b = ring[a + sc];
-    sc = __builtin_bitreverse32(b) >> 26;
-    a = a >= lo + kSlotBytes ? a - kSlotBytes : a + wrap;
+    ix = ring[a + ix] & 63u;
+    a = prev(a);
   }
-  uint32_t o = ooff + ((c_hi - 14u) >> 3);             // output byte of block c_hi, newest first
-  for (uint32_t i = 0; i < nout; i++, o--) {
-    const uint32_t b = ring[a + sc];
-    out[o] = (uint8_t)b;
-    sc = __builtin_bitreverse32(b) >> 26;
-    a = a >= lo + kSlotBytes ? a - kSlotBytes : a + wrap;
+  uint8_t* op = out + ooff + ((c_hi - 14u) >> 3);      // output byte of block c_hi, newest first
+  for (uint32_t i = 0; i < nout; i++) {
+    const uint32_t b = ring[a + ix];
+    *op-- = (uint8_t)b;
+    ix = b & 63u;
+    a = prev(a);
   }
   nbytes = max(nbytes, ((c_hi - 14u) >> 3) + 1u);
 }
 
 // P word of one column from its soft values (a, b) (BM(v, e) = e ? 14-2v : 2v, viterbilut.h)
 __device__ __forceinline__ uint32_t p_word(uint32_t r, uint32_t a, uint32_t b) {
-  const uint32_t a2 = (a & 7u) * 0x02020202u, b2 = (b & 7u) * 0x02020202u;
+  // 2v replicated into 4 bytes with v_perm (v_mul_lo_u32 is a quarter-rate instruction)
+  const uint32_t a2 = __builtin_amdgcn_perm(0u, (a & 7u) << 1, 0u), b2 = __builtin_amdgcn_perm(0u, (b & 7u) << 1, 0u);
   const uint32_t pa = a2 ^ 0x0E0E0000u, pb = a2 ^ 0x0E000E00u;
   return r == 0 ? pa + (b2 ^ 0x0E000E00u) : (r == 1 ? pa : pb);
 }
@@ -307,10 +314,14 @@ __device__ void run_rows(const uint8_t* __restrict__ sp, uint32_t n, Row& R, con
   const uint32_t j1 = l, j2 = 16u + (l & 7u);
   const uint32_t o1 = soft_off<CR>(j1), o2 = soft_off<CR>(j2);
   const uint32_t r1 = j1 % RT::steps, r2 = j2 % RT::steps;
+  // Soft values past the input are clamped to its last byte: the columns they feed lie
+  // beyond R.cols and never reach an output byte.  Unconditional loads (no exec branches)
+  // let the compiler wait for exactly the previous body's loads, not the prefetch.
+  const uint32_t last = n ? n - 1u : 0u;               // rows with no input read byte 0 (harmless)
   auto fetch = [&](uint32_t base, uint32_t o, uint32_t r, uint32_t& a, uint32_t& b) {
-    const uint32_t i = base + o;
-    a = i < n ? sp[i] : 0u;
-    b = (r == 0 && i + 1 < n) ? sp[i + 1] : 0u;
+    const uint32_t i = min(base + o, last);
+    a = sp[i];
+    b = r == 0 ? sp[min(i + 1u, last)] : 0u;
   };
   uint32_t a1, b1, a2, b2;
   fetch(0, o1, r1, a1, b1);
@@ -390,9 +401,9 @@ __global__ __launch_bounds__(256, 4) void k_viterbi3(const uint8_t* __restrict__
     v3::Row Rr = R;
     Rr.live = mine;
     Rr.next = v3::row_next(Rr);
-    if (rate == 0) v3::run_rows<0, DBG>(sp, (uint32_t)n, Rr, K, l, rib, ring, obase, ooff);
-    else if (rate == 1) v3::run_rows<1, DBG>(sp, (uint32_t)n, Rr, K, l, rib, ring, obase, ooff);
-    else v3::run_rows<2, DBG>(sp, (uint32_t)n, Rr, K, l, rib, ring, obase, ooff);
+    if (rate == 0) v3::run_rows<0, DBG>(sp, (uint32_t)max(n, 0), Rr, K, l, rib, ring, obase, ooff);
+    else if (rate == 1) v3::run_rows<1, DBG>(sp, (uint32_t)max(n, 0), Rr, K, l, rib, ring, obase, ooff);
+    else v3::run_rows<2, DBG>(sp, (uint32_t)max(n, 0), Rr, K, l, rib, ring, obase, ooff);
     if (mine) R.nbytes = Rr.nbytes;
   }
   if (valid && l == 0) out_bits[p] = (int32_t)(R.nbytes * 8u);
