@@ -86,6 +86,16 @@ int32_t __ext_wifi_rx_batch(struct complex16* sym, int nsym_total, int32_t* pkt_
                             unsigned char* payload, int payload_len_bits,
                             int32_t* pkt_info, int n_info);
 
+/* The same with ChannelEqualization and PilotTrack between FFT and GetData, i.e. the
+ * receiver order FFT >>> ChannelEqualization(params) >>> PilotTrack >>> GetData >>>
+ * receiveBits of code/WiFi/receiver/receiver.blk:66-71 (OFDM/ChannelEqualization.blk:26-46,
+ * OFDM/PilotTrack.blk:56-249).  chan holds the 64 LTS channel coefficients
+ * (LTECoeffs.channelCoeffs, const.blk:59-61) of each packet: chan[64*i .. 64*i+63],
+ * chan_len >= 64*npkts. */
+int32_t __ext_wifi_rx_eq_batch(struct complex16* sym, int nsym_total, int32_t* pkt_sym_off, int n_off,
+                               struct complex16* chan, int chan_len, unsigned char* payload,
+                               int payload_len_bits, int32_t* pkt_info, int n_info);
+
 /* ================================================================ Part 3: device API */
 
 #define ZRX_OK 0
@@ -132,6 +142,24 @@ int zrx_viterbi_dev(zrx_ctx* ctx, const int8_t* d_soft, const int64_t* d_soft_of
 int zrx_rx_dev(zrx_ctx* ctx, const struct complex16* d_sym, const int64_t* d_sym_off,
                const int32_t* d_nsym, int npkts, int max_nsym, uint8_t* d_payload,
                int32_t* d_info);
+
+/* Full chain with ChannelEqualization + PilotTrack (as __ext_wifi_rx_eq_batch); d_chan: 64
+ * complex16 channel coefficients per packet. */
+int zrx_rx_eq_dev(zrx_ctx* ctx, const struct complex16* d_sym, const int64_t* d_sym_off,
+                  const int32_t* d_nsym, int npkts, int max_nsym, const struct complex16* d_chan,
+                  uint8_t* d_payload, int32_t* d_info);
+
+/* FFT >>> ChannelEqualization >>> PilotTrack over every symbol of every packet (symbol k of
+ * packet i is d_sym[64*(d_sym_off[i]+k) ..], k < d_nsym[i]; k = 0 is the SIGNAL symbol,
+ * which PilotTrack counts as its first).  d_out has d_sym's layout and receives
+ * PilotTrack's 64-bin output. */
+int zrx_ofdm_eq_dev(zrx_ctx* ctx, const struct complex16* d_sym, const int64_t* d_sym_off,
+                    const int32_t* d_nsym, int npkts, const struct complex16* d_chan,
+                    struct complex16* d_out);
+
+/* Host-side copy of the engine's integer trig tables (sinx, cosx: 65536 entries by
+ * unsigned angle; atan2x: 256x256 by (u8)y, (u8)x), csrc/intalglutx.h.  No GPU needed. */
+int zrx_trig_tables(int16_t* sin65536, int16_t* cos65536, int16_t* atan65536);
 
 /* Version / build string. */
 const char* zrx_version(void);

@@ -263,3 +263,70 @@ def tx_packet_freq(payload, mod, coding):
     n = L.zo_tx_data_symbols(_p(payload), payload.size, mod, coding, _p(sub[1:]), maxs)
     assert n > 0
     return sub[: 1 + n].copy()
+
+
+# ---------------------------------------------------------------- ChannelEqualization + PilotTrack
+def _fix_trig(L):
+    for f in ("zo_sin16", "zo_cos16", "zo_atan2_16", "zo_trig_sin_entry", "zo_trig_cos_entry",
+              "zo_trig_atan2_entry"):
+        getattr(L, f).restype = C.c_int16
+    return L
+
+
+def trig_tables():
+    """(sin, cos) over all 65536 unsigned angles and the atan2x table [256*256], int16."""
+    L = _fix_trig(lib())
+    s = np.array([L.zo_trig_sin_entry(r) for r in range(65536)], np.int16)
+    c = np.array([L.zo_trig_cos_entry(r) for r in range(65536)], np.int16)
+    a = np.array([L.zo_trig_atan2_entry(((i >> 8) & 255) - 256 * ((i >> 15) & 1), (i & 255) - 256 * ((i >> 7) & 1))
+                  for i in range(65536)], np.int16)
+    return s, c, a
+
+
+def atan2_16(y, x):
+    return _fix_trig(lib()).zo_atan2_16(C.c_int16(int(y)), C.c_int16(int(x)))
+
+
+def v_mul_complex16(x, y, shift):
+    x = np.ascontiguousarray(x, np.int16).reshape(-1, 2)
+    y = np.ascontiguousarray(y, np.int16).reshape(-1, 2)
+    o = np.zeros_like(x)
+    lib().zo_v_mul_complex16(_p(o), _p(x), _p(y), x.shape[0], int(shift))
+    return o
+
+
+def channel_eq(sym64, coeffs64):
+    s = np.ascontiguousarray(sym64, np.int16).reshape(64, 2)
+    c = np.ascontiguousarray(coeffs64, np.int16).reshape(64, 2)
+    o = np.zeros_like(s)
+    lib().zo_channel_eq(_p(s), _p(c), _p(o))
+    return o
+
+
+def pilot_track(sym64, k):
+    s = np.ascontiguousarray(sym64, np.int16).reshape(64, 2)
+    o = np.zeros_like(s)
+    lib().zo_pilot_track(_p(s), int(k), _p(o))
+    return o
+
+
+def ofdm_eq_symbol(sym64, coeffs64, k):
+    s = np.ascontiguousarray(sym64, np.int16).reshape(64, 2)
+    c = np.ascontiguousarray(coeffs64, np.int16).reshape(64, 2)
+    o = np.zeros_like(s)
+    lib().zo_ofdm_eq_symbol(_p(s), _p(c), int(k), _p(o))
+    return o
+
+
+def rx_batch_time_eq(sym, sym_off, nsym, chan, payload_stride=4096, nthreads=1):
+    """receiver.blk:66-71 over packets: chan int16 [n, 64, 2] channel coefficients."""
+    sym = np.ascontiguousarray(sym, np.int16)
+    sym_off = np.ascontiguousarray(sym_off, np.int64)
+    nsym = np.ascontiguousarray(nsym, np.int32)
+    chan = np.ascontiguousarray(chan, np.int16)
+    n = sym_off.size
+    pay = np.zeros((n, payload_stride), np.uint8)
+    res = (RxResult * n)()
+    lib().zo_rx_batch_time_eq(_p(sym), _p(sym_off), _p(nsym), n, _p(chan), _p(pay), payload_stride, res,
+                              nthreads)
+    return pay, [_res(r) for r in res]

@@ -74,6 +74,29 @@ int zo_rx_packet_time(const zo_c16* sym, int nsym, uint8_t* payload, zo_rx_resul
 /* same, fed frequency-domain data subcarriers (48 per symbol, GetData order) */
 int zo_rx_packet_freq(const zo_c16* sub48, int nsym, uint8_t* payload, zo_rx_result* r);
 
+/* ---- ChannelEqualization + PilotTrack, ziria_oracle_eq.c ---- */
+/* integer trigonometry (csrc/intalgx.h:38-99 over the LUTs of csrc/intalglutx.h) */
+int16_t zo_sin16(int16_t r);                       /* sinx: FP_RAD, pi = 0x8000 */
+int16_t zo_cos16(int16_t r);                       /* cosx */
+int16_t zo_atan2_16(int16_t y, int16_t x);         /* atan2x */
+int16_t zo_trig_sin_entry(int r);                  /* table entries, for the table checks */
+int16_t zo_trig_cos_entry(int r);
+int16_t zo_trig_atan2_entry(int yy, int xx);
+int zo_pilot_sign(int m);                          /* pilotSgn[m] (PilotTrack.blk:70-78) */
+/* __ext_v_mul_complex16 (sora_ext_lib.cpp:2098-2137) */
+void zo_v_mul_complex16(zo_c16* out, const zo_c16* x, const zo_c16* y, int len, int shift);
+/* ChannelEqualization.blk:26-46: bins 0..27, 36..63 times coeffs >> norm_shift (8) */
+void zo_channel_eq(const zo_c16* in64, const zo_c16* coeffs64, zo_c16* out64);
+/* PilotTrack.blk:56-249 on the k-th symbol of a packet (k = 0: the SIGNAL symbol) */
+void zo_pilot_track(const zo_c16* in64, int k, zo_c16* out64);
+/* FFT >>> ChannelEqualization >>> PilotTrack (receiver.blk:66-69) */
+void zo_ofdm_eq_symbol(const zo_c16* sym64, const zo_c16* chan64, int k, zo_c16* out64);
+/* receiver.blk:66-71 on one packet / a batch (chan: 64 coefficients per packet) */
+int zo_rx_packet_time_eq(const zo_c16* sym, int nsym, const zo_c16* chan64, uint8_t* payload, zo_rx_result* r);
+int zo_rx_batch_time_eq(const zo_c16* sym, const int64_t* sym_off, const int32_t* nsym, int npkts,
+                        const zo_c16* chan, uint8_t* payload, int payload_stride, zo_rx_result* res,
+                        int nthreads);
+
 /* Batched Viterbi over packets (same semantics per packet as init + decode of all soft). */
 int zo_viterbi_batch(const int8_t* soft, const int64_t* soft_off, const int32_t* soft_len,
                      const int32_t* frame_len, const int16_t* code_rate, int npkts,

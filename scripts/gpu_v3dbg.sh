@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 for d in ${DBGS:-0 1 2 4 8 16}; do
-  ZRX_V3DBG=$d timeout -k 10 200 python bench.py --steps 5 --warmup 2 --no-cpu > gpurun_out/dbg_$d.log 2>&1; rc=$?
+  ZRX_V3DBG=$d timeout -k 10 200 python bench.py --steps ${STEPS:-5} --warmup 2 --no-cpu > gpurun_out/dbg_$d.log 2>&1; rc=$?
   [ $rc -eq 0 ] || { echo "dbg $d rc=$rc"; tail -5 gpurun_out/dbg_$d.log; exit $rc; }
   python -c "
 import json

@@ -15,7 +15,8 @@ Sources, in order of authority:
      reference (wplc is unavailable), so chain fixtures use the reference FFT + Viterbi
      bricks with the oracle's glue, which is itself pinned by the encdec KATs above.
 
-Usage: python tests/golden/make_golden.py
+Usage: python tests/golden/make_golden.py        (all fixtures)
+       python tests/golden/make_golden.py eq     (ref_eq.npz only)
 """
 import ctypes as C
 import os
@@ -198,15 +199,92 @@ def ref_chain_from_freq(R, sub):
     return pay, int(ok)
 
 
+def eq_vectors(R):
+    """ChannelEqualization + PilotTrack: the reference KATs
+    receiver/tests/test_c_{PilotTrack,ChannelEqualization}.{infile,outfile.ground} as data,
+    hashes and samples of the reference integer trigonometry (csrc/intalgx.h via the
+    compiled reference), per-symbol FFT >>> ChannelEqualization >>> PilotTrack outputs
+    (reference FFT brick, restated .blk glue pinned by those KATs), and a packet batch
+    through a frequency-selective channel decoded with the reference FFT + Viterbi bricks."""
+    import hashlib
+    d = {}
+    T = W + "/receiver/tests/"
+    for tag, name in (("pilot", "test_c_PilotTrack"), ("cheq", "test_c_ChannelEqualization")):
+        g = rd(T + name + ".outfile.ground")
+        n = g.size // 128
+        d[f"{tag}_kat_in"] = rd(T + name + ".infile")[: n * 128].reshape(n, 64, 2).astype(np.int16)
+        d[f"{tag}_kat_out"] = g.reshape(n, 64, 2).astype(np.int16)
+    sv = np.array([R.zref_sin16(int(np.int16(np.uint16(r)))) for r in range(65536)], np.int16)
+    cv = np.array([R.zref_cos16(int(np.int16(np.uint16(r)))) for r in range(65536)], np.int16)
+    d["sin_sha256"] = np.array(hashlib.sha256(sv.tobytes()).hexdigest())
+    d["cos_sha256"] = np.array(hashlib.sha256(cv.tobytes()).hexdigest())
+    grid = np.arange(-300, 301)
+    ag = np.array([[R.zref_atan2_16(int(y), int(x)) for x in grid] for y in grid], np.int16)
+    d["atan2_grid_lo_hi"] = np.array([-300, 300], np.int32)
+    d["atan2_grid_sha256"] = np.array(hashlib.sha256(ag.tobytes()).hexdigest())
+    rng = np.random.default_rng(0xA7A2)
+    edge = np.array([0, 1, -1, 63, 64, -64, -65, 127, 128, -128, -129, 255, -255, 256, -256,
+                     32767, -32768, -32767, 16384, -16384], np.int64)
+    yx = np.concatenate([rng.integers(-32768, 32768, (20000, 2)),
+                         np.stack(np.meshgrid(edge, edge), -1).reshape(-1, 2)])
+    d["atan2_yx"] = yx.astype(np.int16)
+    d["atan2_out"] = np.array([R.zref_atan2_16(int(y), int(x)) for y, x in yx], np.int16)
+    # symbol level: random, extreme and realistic symbols, per-packet coefficients
+    x = np.empty((600, 64, 2), np.int16)
+    x[:200] = rng.integers(-32768, 32768, (200, 64, 2))
+    x[200:300] = rng.choice(np.array([-32768, -32767, 32767, 0, 1, -1], np.int16), (100, 64, 2))
+    x[300:] = rng.integers(-2500, 2500, (300, 64, 2))
+    chan = rng.integers(-32768, 32768, (4, 64, 2)).astype(np.int16)   # 4 packets x 150 symbols
+    chan[1] = rng.integers(-600, 600, (64, 2))
+    chan[2] = rng.choice(np.array([-32768, 32767, 0, 256, -256], np.int16), (64, 2))
+    f = ref_fft64(R, x)
+    out = np.zeros_like(x)
+    L = O.lib()
+    for i in range(600):
+        e = np.zeros((64, 2), np.int16)
+        L.zo_channel_eq(ptr(np.ascontiguousarray(f[i])), ptr(np.ascontiguousarray(chan[i // 150])), ptr(e))
+        o = np.zeros((64, 2), np.int16)
+        L.zo_pilot_track(ptr(e), i % 150, ptr(o))      # symbol index within its packet (wraps at 128)
+        out[i] = o
+    d["eqsym_in"], d["eqsym_chan"], d["eqsym_out"] = x, chan, out
+    d["eqsym_k"] = np.array([i % 150 for i in range(600)], np.int32)
+    # packets through a channel
+    plan = synth.plan_mixed(20, max_len=1200, seed=0xE9) + synth.plan_54mbps(4, 1500)
+    sym, off, nsym, meta, chan = synth.packets_time_eq(plan, seed=0xE90)
+    pays, crcs = [], []
+    for p in range(len(off)):
+        f = ref_fft64(R, sym[off[p]: off[p] + nsym[p]])
+        sub = []
+        for k in range(f.shape[0]):
+            e = np.zeros((64, 2), np.int16)
+            L.zo_channel_eq(ptr(np.ascontiguousarray(f[k])), ptr(np.ascontiguousarray(chan[p])), ptr(e))
+            o = np.zeros((64, 2), np.int16)
+            L.zo_pilot_track(ptr(e), k, ptr(o))
+            sub.append(O.get_data(o))
+        pay, ok = ref_chain_from_freq(R, np.stack(sub))
+        pays.append(pay)
+        crcs.append(ok)
+    d["eq_sym"], d["eq_off"], d["eq_nsym"], d["eq_meta"], d["eq_chan"] = sym, off, nsym, meta, chan
+    d["eq_payload"] = np.concatenate(pays)
+    d["eq_payload_off"] = np.cumsum([0] + [p.size for p in pays]).astype(np.int64)
+    d["eq_crc"] = np.array(crcs, np.int32)
+    return d
+
+
 def main():
     O.build()
     R = O.ref()
     assert R is not None, "reference bricks not built (needs /root/reference)"
+    if sys.argv[1:] == ["eq"]:
+        np.savez_compressed(os.path.join(HERE, "ref_eq.npz"), **eq_vectors(R))
+        print("ref_eq.npz", os.path.getsize(os.path.join(HERE, "ref_eq.npz")))
+        return
     np.savez_compressed(os.path.join(HERE, "ref_kats.npz"), **kats())
     np.savez_compressed(os.path.join(HERE, "ref_tables.npz"), **tables())
     np.savez_compressed(os.path.join(HERE, "ref_fft64.npz"), **fft_vectors(R))
     np.savez_compressed(os.path.join(HERE, "ref_viterbi.npz"), **viterbi_vectors(R))
     np.savez_compressed(os.path.join(HERE, "ref_chain.npz"), **chain_vectors(R))
+    np.savez_compressed(os.path.join(HERE, "ref_eq.npz"), **eq_vectors(R))
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

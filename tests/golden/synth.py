@@ -78,3 +78,51 @@ def packets_time(plan, seed, sigma=4.0, extra_sym=0):
         off += ns
     return (np.concatenate(syms), np.array(offs, np.int64), np.array(nsyms, np.int32),
             np.array(meta, np.int32))
+
+
+def pilot_polarity(k):
+    """+1 / -1 pilot polarity PilotTrack expects on symbol k of a packet (k = 0: SIGNAL),
+    pilotSgn[k == 0 ? 127 : (k-1) % 127] (PilotTrack.blk:70-78, map_ofdm.blk:55-62)."""
+    sc = 127 if k == 0 else (k - 1) % 127
+    return -1.0 if O.lib().zo_pilot_sign(sc) == -1 else 1.0
+
+
+def packets_time_eq(plan, seed, sigma=3.0):
+    """Packets through a frequency-selective channel for the ChannelEqualization +
+    PilotTrack path: per packet a 3-tap channel H and a per-symbol common phase drift plus a
+    small phase slope across subcarriers; pilots carry the 802.11a polarity (TX pilots
+    +, -, +, + on bins 7, 21, 43, 57 before polarity, map_ofdm.blk:40-49, 86-96).  The
+    channel coefficients handed to ChannelEqualization are round(256 / H) (what an ideal
+    LTS stage would give at norm_shift 8).  Returns (sym, sym_off, nsym, meta, chan int16
+    [n, 64, 2])."""
+    rng = np.random.default_rng(seed)
+    syms, offs, nsyms, meta, chans = [], [], [], [], []
+    off = 0
+    b = np.arange(64)
+    sb = np.where(b < 32, b, b - 64).astype(np.float64)
+    for (mod, cod, plen) in plan:
+        pay = rng.integers(0, 256, plen).astype(np.uint8)
+        sub = O.tx_packet_freq(pay, mod, cod).astype(np.float64)       # [nsym,48,2]
+        ns = sub.shape[0]
+        X = np.zeros((ns, 64), np.complex128)
+        X[:, DATA_BINS] = (sub[..., 0] + 1j * sub[..., 1]) / 100.0
+        pol = np.array([pilot_polarity(k) for k in range(ns)])
+        X[:, PILOT_BINS] = 107.0 * pol[:, None] * np.array([1.0, -1.0, 1.0, 1.0])
+        h = rng.normal(0, 0.15, 3) + 1j * rng.normal(0, 0.15, 3)
+        h[0] += 0.7 * np.exp(2j * np.pi * rng.random())
+        H = np.fft.fft(h, 64)
+        phi = rng.uniform(-np.pi, np.pi) + rng.uniform(-0.02, 0.02) * np.arange(ns)
+        slope = rng.uniform(-2e-4, 2e-4) * np.arange(ns)
+        Y = X * H[None, :] * np.exp(1j * (phi[:, None] + slope[:, None] * sb[None, :]))
+        x = np.fft.ifft(Y, axis=1) * 64.0
+        x = x + rng.normal(0.0, sigma, x.shape) + 1j * rng.normal(0.0, sigma, x.shape)
+        t = np.stack([np.rint(x.real), np.rint(x.imag)], -1)
+        syms.append(np.clip(t, -32768, 32767).astype(np.int16))
+        G = 256.0 / H
+        chans.append(np.clip(np.stack([np.rint(G.real), np.rint(G.imag)], -1), -32768, 32767).astype(np.int16))
+        offs.append(off)
+        nsyms.append(ns)
+        meta.append((mod, cod, plen + 4))
+        off += ns
+    return (np.concatenate(syms), np.array(offs, np.int64), np.array(nsyms, np.int32),
+            np.array(meta, np.int32), np.stack(chans))

@@ -64,3 +64,31 @@ def test_shift_right(oracle, ref):
             z = np.zeros_like(x)
             ref.zref_v_shift_right_complex16(_p(z), _p(x), n, sh)
             assert (z == oracle.v_shift_right_complex16(x, sh)).all()
+
+
+def test_trig_exhaustive(oracle, ref):
+    L = oracle.lib()
+    s, c, _ = oracle.trig_tables()
+    r = np.arange(65536).astype(np.uint16).astype(np.int16)
+    rs = np.array([ref.zref_sin16(int(v)) for v in r], np.int16)
+    rc = np.array([ref.zref_cos16(int(v)) for v in r], np.int16)
+    assert (s == rs).all() and (c == rc).all()
+    g = np.arange(-300, 301)
+    for y in g[::7]:
+        for x in g:
+            assert oracle.atan2_16(y, x) == ref.zref_atan2_16(int(y), int(x)), (y, x)
+    rng = np.random.default_rng(31)
+    for y, x in rng.integers(-32768, 32768, (5000, 2)):
+        assert oracle.atan2_16(y, x) == ref.zref_atan2_16(int(y), int(x)), (y, x)
+
+
+def test_v_mul_complex16(oracle, ref):
+    rng = np.random.default_rng(8)
+    for n in (1, 3, 4, 7, 28, 64):
+        for sh in (0, 8, 15, 16):
+            x = rng.integers(-32768, 32768, (n, 2)).astype(np.int16)
+            y = rng.integers(-32768, 32768, (n, 2)).astype(np.int16)
+            x[0] = y[0] = (-32768, -32768)
+            z = np.zeros_like(x)
+            ref.zref_v_mul_complex16(_p(z), _p(x), _p(y), n, sh)
+            assert (z == oracle.v_mul_complex16(x, y, sh)).all(), (n, sh)

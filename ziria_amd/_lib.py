@@ -29,6 +29,7 @@ SIGNATURES = [
     ("__ext_viterbi_batch_decode", C.c_int32,
      [_P, C.c_int, _P, C.c_int, _P, C.c_int, _P, C.c_int, _P, C.c_int, _P, C.c_int]),
     ("__ext_wifi_rx_batch", C.c_int32, [_P, C.c_int, _P, C.c_int, _P, C.c_int, _P, C.c_int]),
+    ("__ext_wifi_rx_eq_batch", C.c_int32, [_P, C.c_int, _P, C.c_int, _P, C.c_int, _P, C.c_int, _P, C.c_int]),
     ("zrx_create", C.c_int, [C.POINTER(C.c_void_p), C.c_int, _P]),
     ("zrx_destroy", C.c_int, [_P]),
     ("zrx_set_stream", C.c_int, [_P, _P]),
@@ -38,6 +39,9 @@ SIGNATURES = [
     ("zrx_fft64_dev", C.c_int, [_P, _P, _P, C.c_int64]),
     ("zrx_viterbi_dev", C.c_int, [_P, _P, _P, _P, C.c_int, _P, _P, _P]),
     ("zrx_rx_dev", C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, _P, _P]),
+    ("zrx_rx_eq_dev", C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, _P, _P, _P]),
+    ("zrx_ofdm_eq_dev", C.c_int, [_P, _P, _P, _P, C.c_int, _P, _P]),
+    ("zrx_trig_tables", C.c_int, [_P, _P, _P]),
     ("zrx_version", C.c_char_p, []),
 ]
 

@@ -129,6 +129,21 @@ def crc_slice4():
     return S
 
 
+def pilot_neg_bits():
+    """pilotSgn (PilotTrack.blk:70-78) as a 128-bit mask, bit m set = -1.  Entry m is the
+    802.11a pilot polarity p_{(m+1) mod 127}, the scrambler output (scramble.blk:28-44) from
+    the all-ones state; both reference tables (also allPilotSgn, map_ofdm.blk:30-38) hold
+    +1 at entry 52 where the standard has p_53 = -1, kept as in the reference."""
+    s, p = [1] * 7, []
+    for _ in range(127):
+        t = s[3] ^ s[0]
+        s = s[1:] + [t]
+        p.append(t)
+    neg = [p[(m + 1) % 127] for m in range(128)]
+    neg[52] = 0
+    return [sum(neg[32 * w + b] << b for b in range(32)) for w in range(4)]
+
+
 def render():
     L = ["// GENERATED by gen_tables.py — do not edit.", "#pragma once", "#include <stdint.h>", ""]
     for N in (16, 64):
@@ -171,6 +186,8 @@ def render():
     L.append("// slicing-by-4 CRC tables: kCrcS4[k][b] = byte table entry advanced by k zero bytes")
     L.append("static constexpr uint32_t kCrcS4[4][256] = {" + ", ".join(
         "{" + ", ".join(f"0x{v:08x}u" for v in S) + "}" for S in S4) + "};")
+    L.append("// pilotSgn (PilotTrack.blk:70-78): bit m of kPilotNeg = entry m is -1")
+    L.append("static constexpr uint32_t kPilotNeg[4] = {" + ", ".join(f"0x{v:08x}u" for v in pilot_neg_bits()) + "};")
     return "\n".join(L) + "\n"
 
 

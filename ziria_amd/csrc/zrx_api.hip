@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <array>
+#include <cmath>
 #include <mutex>
 #include <vector>
 
@@ -50,6 +51,9 @@ struct zrx_ctx {
   int32_t* dec_bits = nullptr;
   int32_t* order = nullptr;       // Viterbi packet order (k_vit_order)
   bool use_order = true;          // ZRX_ORDER=0 turns the ordering off (A/B experiments)
+  // ChannelEqualization / PilotTrack trig tables (built on first use)
+  uint32_t* eq_rot = nullptr;     // 65536 x (cos, -sin) complex16
+  int16_t* eq_atan = nullptr;     // 256 x 256 atan2x_lut
   // per-call externals
   VitStream* vstream = nullptr;
   void* small = nullptr;          // staging for single calls
@@ -86,6 +90,36 @@ __global__ void k_fill_offsets(int64_t* off, int n, int64_t stride) {
 }
 
 static inline int blocks(int64_t n, int per) { return (int)((n + per - 1) / per); }
+
+// Trig tables of ChannelEqualization / PilotTrack: the reference LUTs (csrc/intalglutx.h:23,
+// :3667, :7351) in closed form, with pi written as 3.141593 as their generator did:
+// sinx/cosx[r] = rint(32767 sin/cos(2 r pi' / 65536)), atan2x[(u8)y][(u8)x] =
+// trunc(atan2(y, x) / pi' * 32768).  Checked entry by entry against the reference tables.
+static void make_trig_tables(int16_t* sinv, int16_t* cosv, int16_t* atanv) {
+  const double pi = 3.141593;
+  for (int r = 0; r < 65536; r++) {
+    sinv[r] = (int16_t)std::nearbyint(32767.0 * std::sin((double)r * 2.0 * pi / 65536.0));
+    cosv[r] = (int16_t)std::nearbyint(32767.0 * std::cos((double)r * 2.0 * pi / 65536.0));
+  }
+  for (int i = 0; i < 256; i++)
+    for (int j = 0; j < 256; j++)
+      atanv[(i << 8) | j] = (int16_t)std::trunc(std::atan2((double)(int8_t)i, (double)(int8_t)j) / pi * 32768.0);
+}
+
+static int ensure_eq_tables(zrx_ctx* c) {
+  if (c->eq_rot) return ZRX_OK;
+  std::vector<int16_t> sv(65536), cv(65536), av(65536);
+  make_trig_tables(sv.data(), cv.data(), av.data());
+  std::vector<uint32_t> rot(65536);
+  for (int r = 0; r < 65536; r++)     // build_coeff (PilotTrack.blk:28-50): (cos th, -sin th)
+    rot[r] = (uint32_t)(uint16_t)cv[r] | ((uint32_t)(uint16_t)(int16_t)(-sv[r]) << 16);
+  ZRX_CHECK(hipSetDevice(c->device));
+  ZRX_CHECK(hipMalloc(&c->eq_rot, 65536 * 4));
+  ZRX_CHECK(hipMalloc(&c->eq_atan, 65536 * 2));
+  ZRX_CHECK(hipMemcpy(c->eq_rot, rot.data(), 65536 * 4, hipMemcpyHostToDevice));
+  ZRX_CHECK(hipMemcpy(c->eq_atan, av.data(), 65536 * 2, hipMemcpyHostToDevice));
+  return ZRX_OK;
+}
 
 static void launch_viterbi(zrx_ctx* c, const uint8_t* soft, const int64_t* soft_off, const int32_t* params,
                            int npkts, uint8_t* out, const int64_t* out_off, int32_t* out_bits) {
@@ -138,6 +172,8 @@ int zrx_destroy(zrx_ctx* c) {
   if (!c) return ZRX_OK;
   (void)hipSetDevice(c->device);
   free_ws(c);
+  (void)hipFree(c->eq_rot);
+  (void)hipFree(c->eq_atan);
   (void)hipFree(c->vstream);
   (void)hipFree(c->small);
   for (auto& set : c->evsets)
@@ -216,8 +252,8 @@ int zrx_viterbi_dev(zrx_ctx* c, const int8_t* d_soft, const int64_t* d_soft_off,
   return ZRX_OK;
 }
 
-int zrx_rx_dev(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_sym_off, const int32_t* d_nsym,
-               int npkts, int max_nsym, uint8_t* d_payload, int32_t* d_info) {
+static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_sym_off, const int32_t* d_nsym,
+                    int npkts, int max_nsym, const struct complex16* d_chan, uint8_t* d_payload, int32_t* d_info) {
   if (!c || npkts < 0 || max_nsym < 1) return ZRX_EINVAL;
   if (npkts > c->cap_pkts || max_nsym > c->cap_nsym) {
     std::fprintf(stderr, "ziria_rx: workspace holds %d packets x %d symbols, call zrx_reserve(%d, %d)\n",
@@ -225,6 +261,13 @@ int zrx_rx_dev(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_sym_o
     return ZRX_ENOMEM;
   }
   if (npkts == 0) return ZRX_OK;
+  EqTabs T{nullptr, nullptr};
+  if (d_chan) {
+    const int rc = ensure_eq_tables(c);
+    if (rc) return rc;
+    T = EqTabs{c->eq_rot, c->eq_atan};
+  }
+  const uint32_t* chan = (const uint32_t*)d_chan;
   hipStream_t s = c->stream;
   hipEvent_t* ev = nullptr;
   if (c->timing) {
@@ -236,18 +279,57 @@ int zrx_rx_dev(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_sym_o
     ev = c->evsets[c->nrec++].data();
   }
   if (ev) ZRX_CHECK(hipEventRecord(ev[0], s));
-  k_signal_fft<<<blocks(npkts, 256), 256, 0, s>>>((const uint4*)d_sym, d_sym_off, d_nsym, npkts, (uint4*)c->sig_soft);
+  if (chan)
+    k_signal_fft<true><<<blocks(npkts, 256), 256, 0, s>>>((const uint4*)d_sym, d_sym_off, d_nsym, npkts,
+                                                          (uint4*)c->sig_soft, chan, T);
+  else
+    k_signal_fft<false><<<blocks(npkts, 256), 256, 0, s>>>((const uint4*)d_sym, d_sym_off, d_nsym, npkts,
+                                                           (uint4*)c->sig_soft, chan, T);
   if (ev) ZRX_CHECK(hipEventRecord(ev[1], s));
   k_signal_vit<<<blocks(npkts, 4), 256, 0, s>>>(c->sig_soft, d_nsym, npkts, c->vparams, d_info);
   if (ev) ZRX_CHECK(hipEventRecord(ev[2], s));
-  k_data_fft<<<blocks(npkts, 4), 256, 0, s>>>((const uint4*)d_sym, d_sym_off, c->vparams, npkts, (uint4*)c->soft,
-                                              c->soft_off);
+  if (chan)
+    k_data_fft<true><<<blocks(npkts, 4), 256, 0, s>>>((const uint4*)d_sym, d_sym_off, c->vparams, npkts,
+                                                      (uint4*)c->soft, c->soft_off, chan, T);
+  else
+    k_data_fft<false><<<blocks(npkts, 4), 256, 0, s>>>((const uint4*)d_sym, d_sym_off, c->vparams, npkts,
+                                                       (uint4*)c->soft, c->soft_off, chan, T);
   if (ev) ZRX_CHECK(hipEventRecord(ev[3], s));
   launch_viterbi(c, c->soft, c->soft_off, c->vparams, npkts, c->dec, c->dec_off, c->dec_bits);
   if (ev) ZRX_CHECK(hipEventRecord(ev[4], s));
   k_descramble_crc<<<blocks(npkts, kCrcWaves), 64 * kCrcWaves, 0, s>>>(c->dec, c->dec_bits, d_info, d_payload, npkts);
   if (ev) ZRX_CHECK(hipEventRecord(ev[5], s));
   ZRX_CHECK(hipGetLastError());
+  return ZRX_OK;
+}
+
+int zrx_rx_dev(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_sym_off, const int32_t* d_nsym,
+               int npkts, int max_nsym, uint8_t* d_payload, int32_t* d_info) {
+  return rx_chain(c, d_sym, d_sym_off, d_nsym, npkts, max_nsym, nullptr, d_payload, d_info);
+}
+
+int zrx_rx_eq_dev(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_sym_off, const int32_t* d_nsym,
+                  int npkts, int max_nsym, const struct complex16* d_chan, uint8_t* d_payload, int32_t* d_info) {
+  if (!d_chan && npkts > 0) return ZRX_EINVAL;
+  return rx_chain(c, d_sym, d_sym_off, d_nsym, npkts, max_nsym, d_chan, d_payload, d_info);
+}
+
+int zrx_ofdm_eq_dev(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_sym_off, const int32_t* d_nsym,
+                    int npkts, const struct complex16* d_chan, struct complex16* d_out) {
+  if (!c || npkts < 0 || (npkts > 0 && (!d_sym || !d_sym_off || !d_nsym || !d_chan || !d_out))) return ZRX_EINVAL;
+  if (npkts == 0) return ZRX_OK;
+  const int rc = ensure_eq_tables(c);
+  if (rc) return rc;
+  k_ofdm_eq<<<blocks(npkts, 4), 256, 0, c->stream>>>((const uint4*)d_sym, d_sym_off, d_nsym, npkts,
+                                                     (const uint32_t*)d_chan, EqTabs{c->eq_rot, c->eq_atan},
+                                                     (uint4*)d_out);
+  ZRX_CHECK(hipGetLastError());
+  return ZRX_OK;
+}
+
+int zrx_trig_tables(int16_t* sin65536, int16_t* cos65536, int16_t* atan65536) {
+  if (!sin65536 || !cos65536 || !atan65536) return ZRX_EINVAL;
+  make_trig_tables(sin65536, cos65536, atan65536);
   return ZRX_OK;
 }
 
@@ -449,8 +531,9 @@ int32_t __ext_viterbi_batch_decode(int8_t* soft, int softlen, int32_t* pkt_soft_
   return np;
 }
 
-int32_t __ext_wifi_rx_batch(struct complex16* sym, int nsym_total, int32_t* pkt_sym_off, int n_off,
-                            unsigned char* payload, int payload_len_bits, int32_t* pkt_info, int n_info) {
+static int32_t wifi_rx_batch_impl(struct complex16* sym, int nsym_total, int32_t* pkt_sym_off, int n_off,
+                                  const struct complex16* chan, unsigned char* payload, int payload_len_bits,
+                                  int32_t* pkt_info, int n_info) {
   const int np = n_off - 1;
   if (np < 0 || nsym_total < 0 || n_info < 8 * np || (int64_t)payload_len_bits / 8 < (int64_t)np * kPayloadStride)
     return ZRX_EINVAL;
@@ -471,18 +554,21 @@ int32_t __ext_wifi_rx_batch(struct complex16* sym, int nsym_total, int32_t* pkt_
   const size_t s_sym = ((size_t)nsym_total * 256 + 255) / 256 * 256 + 256;
   const size_t s_off = ((size_t)np * 8 + 255) / 256 * 256, s_ns = ((size_t)np * 4 + 255) / 256 * 256;
   const size_t s_pay = (size_t)np * kPayloadStride, s_info = (size_t)np * 32;
-  uint8_t* d = (uint8_t*)staging(c, s_sym + s_off + s_ns + s_pay + s_info + 1024);
+  const size_t s_chan = chan ? (size_t)np * 256 : 0;
+  uint8_t* d = (uint8_t*)staging(c, s_sym + s_off + s_ns + s_pay + s_info + s_chan + 1024);
   if (!d) return ZRX_ENOMEM;
   uint8_t* d_sym = d;
   int64_t* d_off = (int64_t*)(d + s_sym);
   int32_t* d_ns = (int32_t*)((uint8_t*)d_off + s_off);
   uint8_t* d_pay = (uint8_t*)d_ns + s_ns;
   int32_t* d_info = (int32_t*)(d_pay + s_pay);
+  struct complex16* d_chan = chan ? (struct complex16*)((uint8_t*)d_info + (s_info + 255) / 256 * 256) : nullptr;
+  if (chan) ZRX_CHECK(hipMemcpyAsync(d_chan, chan, s_chan, hipMemcpyHostToDevice, c->stream));
   ZRX_CHECK(hipMemcpyAsync(d_sym, sym, (size_t)nsym_total * 256, hipMemcpyHostToDevice, c->stream));
   ZRX_CHECK(hipMemcpyAsync(d_off, off.data(), (size_t)np * 8, hipMemcpyHostToDevice, c->stream));
   ZRX_CHECK(hipMemcpyAsync(d_ns, ns.data(), (size_t)np * 4, hipMemcpyHostToDevice, c->stream));
   ZRX_CHECK(hipMemsetAsync(d_pay, 0, s_pay, c->stream));
-  rc = zrx_rx_dev(c, (const complex16*)d_sym, d_off, d_ns, np, max_ns, d_pay, d_info);
+  rc = rx_chain(c, (const complex16*)d_sym, d_off, d_ns, np, max_ns, d_chan, d_pay, d_info);
   if (rc) return rc;
   ZRX_CHECK(hipMemcpyAsync(payload, d_pay, s_pay, hipMemcpyDeviceToHost, c->stream));
   ZRX_CHECK(hipMemcpyAsync(pkt_info, d_info, s_info, hipMemcpyDeviceToHost, c->stream));
@@ -490,6 +576,19 @@ int32_t __ext_wifi_rx_batch(struct complex16* sym, int nsym_total, int32_t* pkt_
   int ok = 0;
   for (int i = 0; i < np; i++) ok += pkt_info[8 * i + 4] != 0;
   return ok;
+}
+
+int32_t __ext_wifi_rx_batch(struct complex16* sym, int nsym_total, int32_t* pkt_sym_off, int n_off,
+                            unsigned char* payload, int payload_len_bits, int32_t* pkt_info, int n_info) {
+  return wifi_rx_batch_impl(sym, nsym_total, pkt_sym_off, n_off, nullptr, payload, payload_len_bits, pkt_info, n_info);
+}
+
+int32_t __ext_wifi_rx_eq_batch(struct complex16* sym, int nsym_total, int32_t* pkt_sym_off, int n_off,
+                               struct complex16* chan, int chan_len, unsigned char* payload, int payload_len_bits,
+                               int32_t* pkt_info, int n_info) {
+  const int np = n_off - 1;
+  if (np < 0 || !chan || chan_len < 64 * np) return ZRX_EINVAL;
+  return wifi_rx_batch_impl(sym, nsym_total, pkt_sym_off, n_off, chan, payload, payload_len_bits, pkt_info, n_info);
 }
 
 }  // extern "C"

@@ -133,6 +133,69 @@ __device__ __forceinline__ void demap_deinterleave(const s2* x, const uint32_t* 
   }
 }
 
+// ------------------------------------------------------------------ ChannelEqualization + PilotTrack
+// (receiver.blk:68-69).  Trig tables live in HBM, built once by the host
+// (zrx_api.hip) from the closed forms of the reference LUTs (csrc/intalglutx.h):
+// rot[r] = (cosx(r), -sinx(r)) as one complex16, atan[(u8)y << 8 | (u8)x] = atan2x_lut.
+struct EqTabs {
+  const uint32_t* __restrict__ rot;
+  const int16_t* __restrict__ atan;
+};
+// __ext_v_mul_complex16 (csrc/sora_ext_lib.cpp:2098-2137) on one complex16: im negated in
+// 16 bits, madd_epi16 = v_dot2 (two exact products, 32-bit wrapping sum), >> sh, low 16 bits.
+__device__ __forceinline__ s2 vmul_c16(s2 x, s2 y, int sh) {
+  const s2 a = {x.x, (short)-x.y}, b = {x.y, x.x};
+  const int re = __builtin_amdgcn_sdot2(a, y, 0, false);
+  const int im = __builtin_amdgcn_sdot2(b, y, 0, false);
+  return (s2){(short)(re >> sh), (short)(im >> sh)};
+}
+// atan2x (csrc/intalgx.h:88-99): common right shift until |y|, |x| < 128, then the table.
+__device__ __forceinline__ int atan2_16(int y, int x, const int16_t* __restrict__ tab) {
+  const uint32_t ay = (uint32_t)abs(y), ax = (uint32_t)abs(x);
+  const int ys = ay ? 31 - __builtin_clz(ay) : 0, xs = ax ? 31 - __builtin_clz(ax) : 0;
+  const int sh = max(xs, ys) - 6;
+  if (sh > 0) { y >>= sh; x >>= sh; }
+  return tab[((uint32_t)(y & 0xFF) << 8) | (uint32_t)(x & 0xFF)];
+}
+__device__ __forceinline__ s2 neg16(s2 v) { return (s2){(short)-v.x, (short)-v.y}; }
+// PilotTrack.blk:117-203 on symbol k of a packet (k = 0: SIGNAL; symbol_count starts at 127)
+// from its four equalized pilots (bins 43, 57, 7, 21): the common phase `avg` and the slope
+// `del`; build_coeff (:28-50) then rotates bin b by angle avg + s(b) * del (mod 2^16), with
+// s(b) = b for b in 1..26 and b - 64 for b in 38..63.
+__device__ __forceinline__ void pilot_phase(s2 p1, s2 p2, s2 p3, s2 p4, int k, const int16_t* __restrict__ tab,
+                                            int& avg, int& del) {
+  const int sc = k == 0 ? 127 : (k - 1) % 127;
+  if ((kPilotNeg[sc >> 5] >> (sc & 31)) & 1u) { p1 = neg16(p1); p2 = neg16(p2); p3 = neg16(p3); p4 = neg16(p4); }
+  int th0 = atan2_16(p1.y, p1.x, tab), th1 = atan2_16(p2.y, p2.x, tab);
+  int th2 = atan2_16(p3.y, p3.x, tab), th3 = atan2_16((short)-p4.y, (short)-p4.x, tab);
+  // phase unwrap along the pilots (:186-196)
+  if (th0 - th1 > 32768) th1 += 65536; else if (th1 - th0 > 32768) th1 -= 65536;
+  if (th1 - th2 > 32768) th2 += 65536; else if (th2 - th1 > 32768) th2 -= 65536;
+  if (th2 - th3 > 32768) th3 += 65536; else if (th3 - th2 > 32768) th3 -= 65536;
+  const int a32 = (th0 + th1 + th2 + th3) / 4;
+  avg = a32 >= 32768 ? a32 - 65536 : a32 <= -32768 ? a32 + 65536 : (int)(short)a32;
+  del = (short)(((th2 - th0) / 28 + (th3 - th1) / 28) >> 1);
+}
+__device__ __forceinline__ s2 rot_coeff(int avg, int del, int b, const uint32_t* __restrict__ rot) {
+  const int sb = b < 32 ? b : b - 64;
+  return as_s2(rot[(uint32_t)(avg + sb * del) & 0xFFFFu]);
+}
+// FFT output x (bin b at x[bitrev6(b)]) -> ChannelEqualization -> PilotTrack on the bins
+// GetData keeps (the other bins are never read downstream).  C(b): channel coefficient.
+template <class Coef>
+__device__ __forceinline__ void equalize_data_bins(s2* x, const Coef& C, int k, const EqTabs& T) {
+  const s2 p1 = vmul_c16(x[bitrev6(43)], C(43), 8), p2 = vmul_c16(x[bitrev6(57)], C(57), 8);
+  const s2 p3 = vmul_c16(x[bitrev6(7)], C(7), 8), p4 = vmul_c16(x[bitrev6(21)], C(21), 8);
+  int avg, del;
+  pilot_phase(p1, p2, p3, p4, k, T.atan, avg, del);
+#pragma unroll
+  for (int i = 0; i < 48; i++) {
+    const int b = data_bin(i);
+    const s2 e = vmul_c16(x[bitrev6(b)], C(b), 8);
+    x[bitrev6(b)] = vmul_c16(e, rot_coeff(avg, del, b, T.rot), 15);
+  }
+}
+
 // ------------------------------------------------------------------ wave reductions
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 #pragma unroll

@@ -6,7 +6,9 @@
 //   k_signal_vit     one wave per packet: Viterbi_sig11 (viterbicore.hpp:272-315) +
 //                    parsePLCPHeader (parsePLCPHeader.blk:119-213)
 //   k_data_fft       one wave per packet, lane = data symbol: FFT -> GetData -> DemapLimit ->
-//                    Demap{mod} -> Deinterleave{mod} (Decode.blk:45-60)
+//                    Demap{mod} -> Deinterleave{mod} (Decode.blk:45-60); with EQ, ChannelEqualization
+//                    + PilotTrack after the FFT (receiver.blk:66-71), also in k_signal_fft
+//   k_ofdm_eq        FFT -> ChannelEqualization -> PilotTrack, full 64-bin output
 //   k_viterbi        one wave per packet, lane = trellis state: the whole brick driver loop
 //                    (sora_ext_viterbi.cpp:66-153) with the survivor history in an LDS ring
 //   k_descramble_crc one wave per packet: descrambler (Decode.blk:36-43) + CRC-32 check
@@ -60,9 +62,13 @@ __device__ __forceinline__ void stage_lut(uint32_t* lut) {
 }
 
 // ------------------------------------------------------------------ SIGNAL symbol -> 48 soft
+// EQ: ChannelEqualization (coefficients chan[64p ..]) + PilotTrack between FFT and GetData
+// (receiver.blk:66-71); otherwise the FFT output feeds GetData directly.
+template <bool EQ>
 __global__ __launch_bounds__(256) void k_signal_fft(const uint4* __restrict__ sym, const int64_t* __restrict__ sym_off,
                                                     const int32_t* __restrict__ nsym, int npkts,
-                                                    uint4* __restrict__ sig_soft) {
+                                                    uint4* __restrict__ sig_soft, const uint32_t* __restrict__ chan,
+                                                    EqTabs T) {
   __shared__ uint32_t lut[256];
   stage_lut(lut);
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -72,6 +78,10 @@ __global__ __launch_bounds__(256) void k_signal_fft(const uint4* __restrict__ sy
     s2 x[64];
     load_symbol(sym + sym_off[p] * 16, x);
     fft64_inplace(x);
+    if constexpr (EQ) {
+      const uint32_t* cp = chan + (int64_t)p * 64;
+      equalize_data_bins(x, [cp](int b) { return as_s2(cp[b]); }, 0, T);
+    }
     demap_deinterleave<0>(x, lut, w);
   } else {
 #pragma unroll
@@ -167,14 +177,16 @@ __global__ __launch_bounds__(256) void k_signal_vit(const uint32_t* __restrict__
 }
 
 // ------------------------------------------------------------------ data symbols -> soft
-template <int MOD>
+template <int MOD, bool EQ>
 __device__ __forceinline__ void data_fft_packet(const uint4* __restrict__ sym0, int need, int lane,
-                                                const uint32_t* lut, uint4* __restrict__ dst0) {
+                                                const uint32_t* lut, uint4* __restrict__ dst0,
+                                                const uint32_t* __restrict__ cp, const EqTabs& T) {
   constexpr int NC = ModInfo<MOD>::ncbps;
   for (int k = lane; k < need; k += 64) {
     s2 x[64];
     load_symbol(sym0 + (int64_t)k * 16, x);
     fft64_inplace(x);
+    if constexpr (EQ) equalize_data_bins(x, [cp](int b) { return as_s2(cp[b]); }, k + 1, T);
     uint32_t w[NC / 4];
     demap_deinterleave<MOD>(x, lut, w);
     uint4* dst = dst0 + (int64_t)k * (NC / 16);
@@ -182,24 +194,61 @@ __device__ __forceinline__ void data_fft_packet(const uint4* __restrict__ sym0, 
     for (int q = 0; q < NC / 16; q++) dst[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
   }
 }
+template <bool EQ>
 __global__ __launch_bounds__(256) void k_data_fft(const uint4* __restrict__ sym, const int64_t* __restrict__ sym_off,
                                                   const int32_t* __restrict__ vparams, int npkts,
-                                                  uint4* __restrict__ soft, const int64_t* __restrict__ soft_off) {
+                                                  uint4* __restrict__ soft, const int64_t* __restrict__ soft_off,
+                                                  const uint32_t* __restrict__ chan, EqTabs T) {
   __shared__ uint32_t lut[256];
   stage_lut(lut);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int p = blockIdx.x * 4 + wv;
+  const int p = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wv);   // one packet per wave
   if (p >= npkts) return;
+  const uint32_t* cp = EQ ? chan + (int64_t)p * 64 : nullptr;        // wave-uniform: scalar loads
   const int32_t* vp = vparams + 4 * (int64_t)p;
   const int soft_len = vp[2], mod = vp[3];
   if (soft_len <= 0) return;
   const uint4* s0 = sym + (sym_off[p] + 1) * 16;
   uint4* d0 = soft + soft_off[p] / 16;
   switch (mod) {
-    case 0: data_fft_packet<0>(s0, soft_len / 48, lane, lut, d0); break;
-    case 1: data_fft_packet<1>(s0, soft_len / 96, lane, lut, d0); break;
-    case 2: data_fft_packet<2>(s0, soft_len / 192, lane, lut, d0); break;
-    default: data_fft_packet<3>(s0, soft_len / 288, lane, lut, d0); break;
+    case 0: data_fft_packet<0, EQ>(s0, soft_len / 48, lane, lut, d0, cp, T); break;
+    case 1: data_fft_packet<1, EQ>(s0, soft_len / 96, lane, lut, d0, cp, T); break;
+    case 2: data_fft_packet<2, EQ>(s0, soft_len / 192, lane, lut, d0, cp, T); break;
+    default: data_fft_packet<3, EQ>(s0, soft_len / 288, lane, lut, d0, cp, T); break;
+  }
+}
+
+// FFT >>> ChannelEqualization >>> PilotTrack (receiver.blk:66-69) with PilotTrack's full
+// 64-bin output (bins 0 and 27..37 are zero, PilotTrack.blk:224-227); out has sym's layout.
+// One wave per packet, lane = symbol.
+__global__ __launch_bounds__(256) void k_ofdm_eq(const uint4* __restrict__ sym, const int64_t* __restrict__ sym_off,
+                                                 const int32_t* __restrict__ nsym, int npkts,
+                                                 const uint32_t* __restrict__ chan, EqTabs T, uint4* __restrict__ out) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int p = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wv);
+  if (p >= npkts) return;
+  const uint32_t* cp = chan + (int64_t)p * 64;
+  const int n = nsym[p];
+  for (int k = lane; k < n; k += 64) {
+    const int64_t so = (sym_off[p] + k) * 16;
+    s2 x[64];
+    load_symbol(sym + so, x);
+    fft64_inplace(x);
+    const s2 p1 = vmul_c16(x[bitrev6(43)], as_s2(cp[43]), 8), p2 = vmul_c16(x[bitrev6(57)], as_s2(cp[57]), 8);
+    const s2 p3 = vmul_c16(x[bitrev6(7)], as_s2(cp[7]), 8), p4 = vmul_c16(x[bitrev6(21)], as_s2(cp[21]), 8);
+    int avg, del;
+    pilot_phase(p1, p2, p3, p4, k, T.atan, avg, del);
+    uint32_t o[64];
+#pragma unroll
+    for (int b = 0; b < 64; b++) {
+      if ((b >= 1 && b <= 26) || b >= 38)
+        o[b] = as_u32(vmul_c16(vmul_c16(x[bitrev6(b)], as_s2(cp[b]), 8), rot_coeff(avg, del, b, T.rot), 15));
+      else
+        o[b] = 0u;
+    }
+    uint4* dst = out + so;
+#pragma unroll
+    for (int q = 0; q < 16; q++) dst[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
   }
 }
 

@@ -77,9 +77,11 @@ class RxEngine:
         check(lib().zrx_viterbi_dev(self._h, _ptr(soft), _ptr(soft_off), _ptr(params), n, _ptr(out),
                                     _ptr(out_off), _ptr(out_bits)), "zrx_viterbi_dev")
 
-    def rx(self, sym, sym_off, nsym, max_nsym, payload=None, info=None):
+    def rx(self, sym, sym_off, nsym, max_nsym, payload=None, info=None, chan=None):
         """Full chain.  sym int16 [S,64,2]; sym_off int64 [n] (SIGNAL symbol index);
-        nsym int32 [n].  Returns (payload uint8 [n,4096], info int32 [n,8])."""
+        nsym int32 [n].  With chan (int16 [n,64,2], each packet's LTS channel coefficients)
+        ChannelEqualization + PilotTrack run between FFT and GetData (receiver.blk:66-71).
+        Returns (payload uint8 [n,4096], info int32 [n,8])."""
         n = sym_off.numel()
         assert sym.dtype == torch.int16 and sym_off.dtype == torch.int64 and nsym.dtype == torch.int32
         if payload is None:
@@ -87,6 +89,22 @@ class RxEngine:
         if info is None:
             info = torch.zeros((n, 8), dtype=torch.int32, device=sym.device)
         self._stream()
-        check(lib().zrx_rx_dev(self._h, _ptr(sym), _ptr(sym_off), _ptr(nsym), n, int(max_nsym),
-                               _ptr(payload), _ptr(info)), "zrx_rx_dev")
+        if chan is None:
+            check(lib().zrx_rx_dev(self._h, _ptr(sym), _ptr(sym_off), _ptr(nsym), n, int(max_nsym),
+                                   _ptr(payload), _ptr(info)), "zrx_rx_dev")
+        else:
+            assert chan.dtype == torch.int16 and chan.is_contiguous() and chan.numel() == 128 * n
+            check(lib().zrx_rx_eq_dev(self._h, _ptr(sym), _ptr(sym_off), _ptr(nsym), n, int(max_nsym),
+                                      _ptr(chan), _ptr(payload), _ptr(info)), "zrx_rx_eq_dev")
         return payload, info
+
+    def ofdm_eq(self, sym, sym_off, nsym, chan, out=None):
+        """FFT >>> ChannelEqualization >>> PilotTrack of every symbol of every packet
+        (PilotTrack's full 64-bin output, same layout as sym)."""
+        n = sym_off.numel()
+        assert sym.dtype == torch.int16 and chan.dtype == torch.int16 and chan.numel() == 128 * n
+        out = torch.zeros_like(sym) if out is None else out
+        self._stream()
+        check(lib().zrx_ofdm_eq_dev(self._h, _ptr(sym), _ptr(sym_off), _ptr(nsym), n, _ptr(chan), _ptr(out)),
+              "zrx_ofdm_eq_dev")
+        return out

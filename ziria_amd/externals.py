@@ -126,3 +126,19 @@ def wifi_rx_batch(sym, pkt_sym_off):
     if rc < 0:
         raise ZiriaRxError(f"__ext_wifi_rx_batch failed ({rc})")
     return pay[:n], {k: info[:n, i].copy() for i, k in enumerate(INFO_FIELDS)}, int(rc)
+
+
+def wifi_rx_eq_batch(sym, pkt_sym_off, chan):
+    """wifi_rx_batch with ChannelEqualization + PilotTrack (receiver.blk:66-71); chan int16
+    [n, 64, 2]: each packet's LTS channel coefficients."""
+    x = np.ascontiguousarray(sym, dtype=np.int16).reshape(-1, 64, 2)
+    off = np.ascontiguousarray(pkt_sym_off, np.int32)
+    ch = np.ascontiguousarray(chan, np.int16).reshape(-1, 64, 2)
+    n = off.size - 1
+    pay = np.zeros((max(n, 1), PAYLOAD_STRIDE), np.uint8)
+    info = np.zeros((max(n, 1), 8), np.int32)
+    rc = lib().__ext_wifi_rx_eq_batch(_p(x), x.shape[0], _p(off), off.size, _p(ch), ch.shape[0] * 64,
+                                      _p(pay), pay.size * 8, _p(info), info.size)
+    if rc < 0:
+        raise ZiriaRxError(f"__ext_wifi_rx_eq_batch failed ({rc})")
+    return pay[:n], {k: info[:n, i].copy() for i, k in enumerate(INFO_FIELDS)}, int(rc)

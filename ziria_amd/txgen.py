@@ -120,39 +120,85 @@ def packets_freq(payloads, mod, coding, device="cpu"):
     return out
 
 
-def to_time(freq, sigma, gen, atten=100.0):
-    """freq int64 [n, S, 48, 2] -> time-domain int16 [n, S, 64, 2] (Appendix E channel)."""
+def pilot_polarity(S):
+    """+1/-1 pilot polarity of symbols 0..S-1 of a packet (0 = SIGNAL) as PilotTrack reads
+    it: pilotSgn[k == 0 ? 127 : (k-1) % 127] (PilotTrack.blk:70-78, map_ofdm.blk:55-62), the
+    802.11a sequence with the reference tables' +1 at entry 52."""
+    s, p = [1] * 7, []
+    for _ in range(127):
+        t = s[3] ^ s[0]
+        s = s[1:] + [t]
+        p.append(t)
+    sgn = [-1.0 if p[(m + 1) % 127] else 1.0 for m in range(128)]
+    sgn[52] = 1.0
+    return np.array([sgn[127 if k == 0 else (k - 1) % 127] for k in range(S)], np.float32)
+
+
+def to_time(freq, sigma, gen, atten=100.0, channel=False):
+    """freq int64 [n, S, 48, 2] -> time-domain int16 [n, S, 64, 2] (Appendix E channel).
+    channel=True: pilots with the 802.11a polarity (+,-,+,+ on bins 7,21,43,57,
+    map_ofdm.blk:40-49), a 3-tap channel H per packet, a common phase drift per symbol and a
+    small phase slope across subcarriers; returns (sym, chan) with chan int16 [n,64,2] =
+    round(256 / H), the coefficients ChannelEqualization (norm_shift 8) takes."""
     n, S = freq.shape[:2]
     dev = freq.device
     X = torch.zeros((n, S, 64), dtype=torch.complex64, device=dev)
     bins = torch.tensor(DATA_BINS, device=dev)
     X[:, :, bins] = torch.complex(freq[..., 0].float(), freq[..., 1].float()) / atten
-    pil = (torch.randint(0, 2, (n, S, 4), generator=gen, device=dev) * 2 - 1).float() * 107.0
-    X[:, :, torch.tensor(PILOT_BINS, device=dev)] = torch.complex(pil, torch.zeros_like(pil))
+    pbins = torch.tensor(PILOT_BINS, device=dev)
+    if channel:
+        pol = torch.from_numpy(pilot_polarity(S)).to(dev)
+        pil = 107.0 * pol[None, :, None] * torch.tensor([1.0, -1.0, 1.0, 1.0], device=dev)
+        X[:, :, pbins] = torch.complex(pil.expand(n, S, 4).contiguous(), torch.zeros((n, S, 4), device=dev))
+        h = torch.complex(torch.randn((n, 3), generator=gen, device=dev), torch.randn((n, 3), generator=gen, device=dev)) * 0.15
+        ph0 = torch.rand((n,), generator=gen, device=dev) * 2 * np.pi
+        h[:, 0] += 0.7 * torch.exp(torch.complex(torch.zeros_like(ph0), ph0))
+        H = torch.fft.fft(h, n=64, dim=-1)                                   # [n, 64]
+        k = torch.arange(S, device=dev, dtype=torch.float32)
+        drift = (torch.rand((n, 1), generator=gen, device=dev) * 2 - 1) * 0.02
+        slope = (torch.rand((n, 1), generator=gen, device=dev) * 2 - 1) * 2e-4
+        b = torch.arange(64, device=dev)
+        sb = torch.where(b < 32, b, b - 64).float()
+        ang = (drift * k)[:, :, None] + (slope * k)[:, :, None] * sb[None, None, :]
+        X = X * H[:, None, :] * torch.exp(torch.complex(torch.zeros_like(ang), ang))
+        G = 256.0 / H
+        chan = torch.clamp(torch.round(torch.stack([G.real, G.imag], -1)), -32768, 32767).to(torch.int16)
+    else:
+        pil = (torch.randint(0, 2, (n, S, 4), generator=gen, device=dev) * 2 - 1).float() * 107.0
+        X[:, :, pbins] = torch.complex(pil, torch.zeros_like(pil))
     x = torch.fft.ifft(X, dim=-1) * 64.0
     t = torch.stack([x.real, x.imag], -1)
     if sigma > 0:
         t = t + sigma * torch.randn(t.shape, generator=gen, device=dev)
-    return torch.clamp(torch.round(t), -32768, 32767).to(torch.int16)
+    t = torch.clamp(torch.round(t), -32768, 32767).to(torch.int16)
+    return (t, chan) if channel else t
 
 
-def make_batch(n, mod=3, coding=2, payload_len=1500, sigma=4.0, seed=0x5EED, device="cpu", chunk=2048):
+def make_batch(n, mod=3, coding=2, payload_len=1500, sigma=4.0, seed=0x5EED, device="cpu", chunk=2048,
+               channel=False):
     """BASELINE config 3 shape by default: n packets of payload_len bytes at (mod, coding).
     Returns dict(sym int16 [n*S,64,2], sym_off int64 [n], nsym int32 [n], payload uint8
-    [n, L], max_nsym)."""
+    [n, L], max_nsym); channel=True adds the channel of to_time and chan int16 [n,64,2]."""
     rng = np.random.default_rng(seed)
     gen = torch.Generator(device=device)
     gen.manual_seed(seed)
     payloads = rng.integers(0, 256, (n, payload_len), dtype=np.uint8)
-    syms = []
+    syms, chans = [], []
     for a in range(0, n, chunk):
         f = packets_freq(payloads[a:a + chunk], mod, coding, device)
-        syms.append(to_time(f, sigma, gen).reshape(-1, 64, 2))
+        t = to_time(f, sigma, gen, channel=channel)
+        if channel:
+            t, c = t
+            chans.append(c)
+        syms.append(t.reshape(-1, 64, 2))
     S = 1 + n_data_symbols(mod, coding, payload_len)
     sym = torch.cat(syms, 0)
-    return dict(sym=sym, sym_off=torch.arange(n, dtype=torch.int64, device=device) * S,
-                nsym=torch.full((n,), S, dtype=torch.int32, device=device), payload=payloads,
-                max_nsym=S, mod=mod, coding=coding, payload_len=payload_len)
+    d = dict(sym=sym, sym_off=torch.arange(n, dtype=torch.int64, device=device) * S,
+             nsym=torch.full((n,), S, dtype=torch.int32, device=device), payload=payloads,
+             max_nsym=S, mod=mod, coding=coding, payload_len=payload_len)
+    if channel:
+        d["chan"] = torch.cat(chans, 0).contiguous()
+    return d
 
 
 MCS8 = [(0, 0), (0, 2), (1, 0), (1, 2), (2, 0), (2, 2), (3, 1), (3, 2)]
