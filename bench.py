@@ -64,6 +64,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall time budget of the CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--config", type=int, default=3, choices=[2, 3, 5])
+    ap.add_argument("--eq", action="store_true",
+                    help="config 3 through a channel, with ChannelEqualization + PilotTrack (SURVEY §8f row 1)")
     args = ap.parse_args()
     if args.config == 2:
         return bench_viterbi_only(args)
@@ -84,7 +86,9 @@ def main():
 
     # ---------------------------------------------------------------- workload (HBM-resident)
     b = txgen.make_batch(args.npkts, mod=3, coding=2, payload_len=args.payload,
-                         seed=0x5EED + 7919 * rank, device=dev)
+                         seed=0x5EED + 7919 * rank, device=dev, channel=args.eq,
+                         sigma=2.0 if args.eq else 4.0)
+    chan = b.get("chan")
     n, S = args.npkts, b["max_nsym"]
     eng = RxEngine(local)
     eng.reserve(n, S)
@@ -92,7 +96,7 @@ def main():
     info = torch.zeros((n, 8), dtype=torch.int32, device=dev)
 
     def step():
-        eng.rx(b["sym"], b["sym_off"], b["nsym"], S, payload, info)
+        eng.rx(b["sym"], b["sym_off"], b["nsym"], S, payload, info, chan=chan)
 
     for _ in range(args.warmup):
         step()
@@ -111,7 +115,7 @@ def main():
     elapsed = node.max_over_ranks(t1 - t0, device=dev)
 
     # ---------------------------------------------------------------- bit-exact self-check + gather
-    ok, bits, match = node.counts(info, payload=payload, expected=b["payload"])
+    ok, bits, match = node.counts(info, payload=payload, expected=b["payload"], crc_ok_only=args.eq)
     torch.cuda.synchronize()
     tg = time.perf_counter()
     ok_all, bits_all, match_all, _ = node.combine(ok, bits, match, payload[:, :args.payload].contiguous(),
@@ -132,7 +136,7 @@ def main():
     # ---------------------------------------------------------------- CPU baseline (rank 0, N=1)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(b, args.payload, args.cpu_seconds)
+        cpu = cpu_baseline(b, args.payload, args.cpu_seconds, chan)
 
     if rank == 0:
         line = {
@@ -147,10 +151,12 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int16+u8",
-            "data": "synthetic (txgen: random payloads, TX restated from transmitter.blk, AWGN sigma=4)",
-            "config": {"workload": f"config3: {n} packets/GPU x {args.payload} B payload @ 54 Mbps "
-                                   f"(64-QAM r3/4), {S} CP-removed complex16 OFDM symbols each, "
-                                   "time-domain input resident in HBM",
+            "data": ("synthetic (txgen: random payloads, TX restated from transmitter.blk, "
+                     + ("3-tap channel + phase drift, AWGN sigma=2)" if args.eq else "AWGN sigma=4)")),
+            "config": {"workload": f"config3{'+eq' if args.eq else ''}: {n} packets/GPU x {args.payload} B payload "
+                                   f"@ 54 Mbps (64-QAM r3/4), {S} CP-removed complex16 OFDM symbols each, "
+                                   "time-domain input resident in HBM"
+                                   + (", FFT >>> ChannelEqualization >>> PilotTrack >>> GetData" if args.eq else ""),
                        "packets_per_gpu": n, "payload_bytes": args.payload, "symbols_per_packet": S,
                        "parallelism": f"packet-sharded x{world}"},
             "bit_exact_check": {"crc_pass": ok_all, "packets": n * world, "payload_match": match_all == world},
@@ -158,12 +164,12 @@ def main():
             "roofline": {"kernel": "k_viterbi3 (data Viterbi)", "bound": "valu",
                          "achieved": round(achieved_tops, 3), "peak": round(VALU_PEAK_TOPS, 1),
                          "unit": "Tops/s", "frac": round(achieved_tops / VALU_PEAK_TOPS, 4),
-                         "traffic": traffic_for("k_viterbi3", n),
+                         "traffic": None if args.eq else traffic_for("k_viterbi3", n),
                          "units": f"{OPS_PER_DECODED_BIT} int ops per decoded bit x {decoded_bits} bits/launch"},
             "roofline_fft": {"kernel": "k_data_fft (FFT64+GetData+demap+deinterleave)", "bound": "hbm",
                              "achieved": round(fft_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(fft_gbs / HBM_PEAK_GBS, 4),
-                             "traffic": traffic_for("k_data_fft", n),
+                             "traffic": None if args.eq else traffic_for("k_data_fft", n),
                              "units": f"544 B per data symbol x {n * nsym_data} symbols/launch"},
             "gather_ms": round(gather_ms, 3),
             "cpu_baseline": cpu,
@@ -279,7 +285,7 @@ def bench_mixed(args):
     }), flush=True)
 
 
-def cpu_baseline(b, payload_len, seconds):
+def cpu_baseline(b, payload_len, seconds, chan=None):
     """The oracle (scalar C restatement, "port") on the host cores this process may use,
     packet-parallel with pthreads, over chunks of the same packets until `seconds` of wall
     time have passed."""
@@ -288,13 +294,17 @@ def cpu_baseline(b, payload_len, seconds):
     sym = b["sym"].cpu().numpy()
     off_all = b["sym_off"].cpu().numpy()
     ns_all = b["nsym"].cpu().numpy()
+    ch_all = chan.cpu().numpy() if chan is not None else None
     chunk = 1024
     done = ok = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         lo = done % off_all.size
         hi = min(lo + chunk, off_all.size)
-        _, res = O.rx_batch_time(sym, off_all[lo:hi], ns_all[lo:hi], nthreads=threads)
+        if ch_all is None:
+            _, res = O.rx_batch_time(sym, off_all[lo:hi], ns_all[lo:hi], nthreads=threads)
+        else:
+            _, res = O.rx_batch_time_eq(sym, off_all[lo:hi], ns_all[lo:hi], ch_all[lo:hi], nthreads=threads)
         ok += sum(r["crc_ok"] for r in res)
         done += hi - lo
     dt = time.perf_counter() - t0

@@ -96,7 +96,7 @@ def test_eq_chain_large_54mbps_vs_oracle(engine, oracle):
     assert (info[:, 4] == np.array([r["crc_ok"] for r in ores])).all()
     assert (pay[:, :1500] == opay[:, :1500]).all()
     ok = info[:, 4] == 1
-    assert ok.sum() > 2000 and (pay[ok, :1500] == b["payload"][ok]).all()
+    assert ok.sum() > 1900 and (pay[ok, :1500] == b["payload"][ok]).all()
 
 
 def test_eq_rejects_missing_coefficients(engine):

@@ -21,16 +21,18 @@ def shard_range(npkts, world, rank):
     return start, start + base + (1 if rank < extra else 0)
 
 
-def counts(info, payload_len=None, payload=None, expected=None):
+def counts(info, payload_len=None, payload=None, expected=None, crc_ok_only=False):
     """Per-rank totals from an info tensor [n, 8] (ziria_rx.h layout): CRC-pass count,
-    CRC-checked payload bits, and 1 if `payload` equals `expected` (when given)."""
+    CRC-checked payload bits, and 1 if `payload` equals `expected` (when given; on the
+    CRC-passing packets only with crc_ok_only)."""
     crc_ok = info[:, 4] == 1
     ok = int(crc_ok.sum())
     bits = int(((info[:, 2].to(torch.int64) - 4) * 8 * crc_ok).sum())
     match = 1
     if expected is not None:
         exp = torch.as_tensor(expected, device=payload.device)
-        match = int(bool((payload[:, :exp.shape[1]] == exp).all()))
+        eq = payload[:, :exp.shape[1]] == exp
+        match = int(bool(eq[crc_ok].all() if crc_ok_only else eq.all()))
     return ok, bits, match
 
 

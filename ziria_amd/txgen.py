@@ -150,7 +150,7 @@ def to_time(freq, sigma, gen, atten=100.0, channel=False):
         pol = torch.from_numpy(pilot_polarity(S)).to(dev)
         pil = 107.0 * pol[None, :, None] * torch.tensor([1.0, -1.0, 1.0, 1.0], device=dev)
         X[:, :, pbins] = torch.complex(pil.expand(n, S, 4).contiguous(), torch.zeros((n, S, 4), device=dev))
-        h = torch.complex(torch.randn((n, 3), generator=gen, device=dev), torch.randn((n, 3), generator=gen, device=dev)) * 0.15
+        h = torch.complex(torch.randn((n, 3), generator=gen, device=dev), torch.randn((n, 3), generator=gen, device=dev)) * 0.1
         ph0 = torch.rand((n,), generator=gen, device=dev) * 2 * np.pi
         h[:, 0] += 0.7 * torch.exp(torch.complex(torch.zeros_like(ph0), ph0))
         H = torch.fft.fft(h, n=64, dim=-1)                                   # [n, 64]
