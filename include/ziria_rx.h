@@ -96,6 +96,19 @@ int32_t __ext_wifi_rx_eq_batch(struct complex16* sym, int nsym_total, int32_t* p
                                struct complex16* chan, int chan_len, unsigned char* payload,
                                int payload_len_bits, int32_t* pkt_info, int n_info);
 
+/* receiver() of code/WiFi/receiver/receiver.blk:57-72 once per capture: capture i =
+ * samples[cap_off[i] .. cap_off[i+1]) (complex16, the receiver's input; downsample != 0
+ * first applies downSample.blk, keeping the odd samples of every 8).  removeDC >>>
+ * cca(1000) finds the preamble (cca/cca_tufv.blk), LTS (OFDM/LTS.blk) estimates the channel,
+ * DataSymbol strips the cyclic prefix, then the decode chain runs with ChannelEqualization
+ * and PilotTrack.  payload / pkt_info as __ext_wifi_rx_batch; det[8*i ..] = {detected,
+ * noSamples, shift, energy, noise, maxCorr (CCAParams, const.blk:51-57), samples consumed by
+ * the detection, first data sample}.  Returns the number of captures with a detected
+ * packet whose CRC passed. */
+int32_t __ext_wifi_rx_stream_batch(struct complex16* samples, int nsamples, int32_t* cap_off, int n_off,
+                                   int downsample, unsigned char* payload, int payload_len_bits,
+                                   int32_t* pkt_info, int n_info, int32_t* det, int n_det);
+
 /* ================================================================ Part 3: device API */
 
 #define ZRX_OK 0
@@ -156,6 +169,17 @@ int zrx_rx_eq_dev(zrx_ctx* ctx, const struct complex16* d_sym, const int64_t* d_
 int zrx_ofdm_eq_dev(zrx_ctx* ctx, const struct complex16* d_sym, const int64_t* d_sym_off,
                     const int32_t* d_nsym, int npkts, const struct complex16* d_chan,
                     struct complex16* d_out);
+
+/* receiver() per capture on device buffers (as __ext_wifi_rx_stream_batch); d_cap_off int64,
+ * d_cap_len int32 in input samples, max_len >= every d_cap_len (sizes the symbol staging,
+ * which grows on first use), d_det 8 int32 per capture. */
+int zrx_rx_stream_dev(zrx_ctx* ctx, const struct complex16* d_samples, const int64_t* d_cap_off,
+                      const int32_t* d_cap_len, int ncap, int max_len, int downsample,
+                      uint8_t* d_payload, int32_t* d_info, int32_t* d_det);
+
+/* Host-side copy of the STS correlation pattern of cca (cca_tufv.blk:80-98), 16 x 16
+ * complex16.  No GPU needed. */
+int zrx_cca_pattern(int16_t* pattern512);
 
 /* Host-side copy of the engine's integer trig tables (sinx, cosx: 65536 entries by
  * unsigned angle; atan2x: 256x256 by (u8)y, (u8)x), csrc/intalglutx.h.  No GPU needed. */

@@ -330,3 +330,50 @@ def rx_batch_time_eq(sym, sym_off, nsym, chan, payload_stride=4096, nthreads=1):
     lib().zo_rx_batch_time_eq(_p(sym), _p(sym_off), _p(nsym), n, _p(chan), _p(pay), payload_stride, res,
                               nthreads)
     return pay, [_res(r) for r in res]
+
+
+
+# ---------------------------------------------------------------- RX front end
+class CCA(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("noSamples", "shift", "energy", "noise", "maxCorr")]
+
+
+def ifft64(x):
+    x = np.ascontiguousarray(x, np.int16).reshape(64, 2)
+    o = np.zeros_like(x)
+    lib().zo_ifft64(_p(x), _p(o))
+    return o
+
+
+def downsample(x):
+    x = np.ascontiguousarray(x, np.int16).reshape(-1, 2)
+    o = np.zeros_like(x)
+    n = lib().zo_downsample(_p(x), x.shape[0], _p(o))
+    return o[:n].copy()
+
+
+def cca_pattern():
+    o = np.zeros((256, 2), np.int16)
+    lib().zo_cca_pattern(_p(o))
+    return o
+
+
+def lts_coeffs(xp144, shift, amp, sora_compat=False):
+    xp = np.ascontiguousarray(xp144, np.int16).reshape(144, 2)
+    o = np.zeros((64, 2), np.int16)
+    lib().zo_lts_coeffs_mode(_p(xp), int(shift), int(amp), _p(o), 1 if sora_compat else 0)
+    return o
+
+
+def rx_stream(x):
+    """receiver() on one stream (after any downSample): (payload, result dict, det dict,
+    coeffs [64,2], data_start) or None when no packet is detected."""
+    x = np.ascontiguousarray(x, np.int16).reshape(-1, 2)
+    pay = np.zeros(4200, np.uint8)
+    r, det, d0 = RxResult(), CCA(), C.c_int()
+    co = np.zeros((64, 2), np.int16)
+    ret = lib().zo_rx_stream(_p(x), x.shape[0], _p(pay), C.byref(r), C.byref(det), _p(co), C.byref(d0))
+    d = _res(r)
+    d["ret"] = ret
+    dd = {k: getattr(det, k) for k, _ in CCA._fields_}
+    return pay[: max(d["len"] - 4, 0)].copy(), d, dd, co, d0.value

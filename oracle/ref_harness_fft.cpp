@@ -23,3 +23,6 @@ extern "C" __attribute__((visibility("default")))
 void zref_v_mul_complex16(struct complex16* out, struct complex16* x, struct complex16* y, int len, int shift) {
   __ext_v_mul_complex16(out, len, x, len, y, len, shift);
 }
+// IFFT<64> brick (csrc/sora_ext_lib.cpp:2828), for the STS pattern of cca_tufv.blk
+extern "C" __attribute__((visibility("default")))
+void zref_sora_ifft64(struct complex16* out, struct complex16* in) { __ext_sora_ifft(out, 64, in, 64); }

@@ -97,6 +97,21 @@ int zo_rx_batch_time_eq(const zo_c16* sym, const int64_t* sym_off, const int32_t
                         const zo_c16* chan, uint8_t* payload, int payload_stride, zo_rx_result* res,
                         int nthreads);
 
+/* ---- RX front end, ziria_oracle_fe.c ---- */
+typedef struct { int32_t noSamples; int32_t shift; int32_t energy; int32_t noise; int32_t maxCorr; } zo_cca;  /* const.blk:51-57 */
+void zo_ifft64(const zo_c16* in, zo_c16* out);                     /* IFFT<64>, csrc/ifft_r4difx.hpp */
+int  zo_downsample(const zo_c16* in, int n, zo_c16* out);          /* downSample.blk: returns n/8*4 */
+void zo_cca_pattern(zo_c16* pattern256);                           /* cca_tufv.blk:50-98 */
+int  zo_remove_dc(const zo_c16* x, int n, zo_c16* y);              /* removeDC.blk:25-85 */
+/* removeDC >>> cca(threshold) (receiver.blk:38-40); 0 = detected */
+int  zo_detect_preamble(const zo_c16* x, int n, int32_t energy_threshold, zo_cca* det, int* consumed);
+int  zo_lts_agc_shift(int32_t amp);                                /* LTS.blk:146 */
+void zo_lts_coeffs(const zo_c16* xp144, int shift, int32_t amp, zo_c16* coeffs64);   /* LTS.blk:113-203 */
+void zo_lts_coeffs_mode(const zo_c16* xp144, int shift, int32_t amp, zo_c16* coeffs64, int sora_compat);
+/* receiver() (receiver.blk:57-72) on one stream */
+int  zo_rx_stream(const zo_c16* x, int n, uint8_t* payload, zo_rx_result* r, zo_cca* det, zo_c16* coeffs64,
+                  int* data_start);
+
 /* Batched Viterbi over packets (same semantics per packet as init + decode of all soft). */
 int zo_viterbi_batch(const int8_t* soft, const int64_t* soft_off, const int32_t* soft_len,
                      const int32_t* frame_len, const int16_t* code_rate, int npkts,

@@ -17,6 +17,7 @@ Sources, in order of authority:
 
 Usage: python tests/golden/make_golden.py        (all fixtures)
        python tests/golden/make_golden.py eq     (ref_eq.npz only)
+       python tests/golden/make_golden.py fe     (ref_fe.npz only)
 """
 import ctypes as C
 import os
@@ -271,10 +272,44 @@ def eq_vectors(R):
     return d
 
 
+def fe_vectors(R):
+    """RX front end: the reference's end-to-end KATs
+    code/WiFi/tests/test_rx.* and test_real_rx.* (captures -> decoded bytes) and the block
+    KATs receiver/tests/test_c_{RemoveDC,DownSample,DataSymbol,LTS} as data, plus IFFT64
+    vectors of the compiled reference brick (the STS pattern of cca_tufv.blk)."""
+    d = {}
+    for tag, name in (("rx", "test_rx"), ("real", "test_real_rx")):
+        d[f"{tag}_in"] = rd(W + f"/tests/{name}.infile").reshape(-1, 2).astype(np.int16)
+        d[f"{tag}_out"] = rd(W + f"/tests/{name}.outfile.ground").astype(np.int8).view(np.uint8)
+    T = W + "/receiver/tests/"
+    for tag, name in (("rdc", "test_c_RemoveDC"), ("ds", "test_c_DownSample"), ("dsym", "test_c_DataSymbol"),
+                      ("lts", "test_c_LTS")):
+        x = rd(T + name + ".infile")
+        d[f"{tag}_in"] = x[: x.size // 2 * 2].reshape(-1, 2).astype(np.int16)
+        d[f"{tag}_out"] = rd(T + name + ".outfile.ground").reshape(-1, 2).astype(np.int16)
+    rng = np.random.default_rng(0x1FF7)
+    x = np.empty((200, 64, 2), np.int16)
+    x[:100] = rng.integers(-32768, 32768, (100, 64, 2))
+    x[100:150] = rng.choice(np.array([-32768, 32767, 0, 1, -1], np.int16), (50, 64, 2))
+    x[150:] = rng.integers(-3000, 3000, (50, 64, 2))
+    out = np.zeros_like(x)
+    for i in range(200):
+        xi = np.ascontiguousarray(x[i])
+        oi = np.zeros_like(xi)
+        R.zref_sora_ifft64(ptr(oi), ptr(xi))
+        out[i] = oi
+    d["ifft_in"], d["ifft_out"] = x, out
+    return d
+
+
 def main():
     O.build()
     R = O.ref()
     assert R is not None, "reference bricks not built (needs /root/reference)"
+    if sys.argv[1:] == ["fe"]:
+        np.savez_compressed(os.path.join(HERE, "ref_fe.npz"), **fe_vectors(R))
+        print("ref_fe.npz", os.path.getsize(os.path.join(HERE, "ref_fe.npz")))
+        return
     if sys.argv[1:] == ["eq"]:
         np.savez_compressed(os.path.join(HERE, "ref_eq.npz"), **eq_vectors(R))
         print("ref_eq.npz", os.path.getsize(os.path.join(HERE, "ref_eq.npz")))
@@ -285,6 +320,7 @@ def main():
     np.savez_compressed(os.path.join(HERE, "ref_viterbi.npz"), **viterbi_vectors(R))
     np.savez_compressed(os.path.join(HERE, "ref_chain.npz"), **chain_vectors(R))
     np.savez_compressed(os.path.join(HERE, "ref_eq.npz"), **eq_vectors(R))
+    np.savez_compressed(os.path.join(HERE, "ref_fe.npz"), **fe_vectors(R))
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

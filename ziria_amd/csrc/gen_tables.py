@@ -186,6 +186,10 @@ def render():
     L.append("// slicing-by-4 CRC tables: kCrcS4[k][b] = byte table entry advanced by k zero bytes")
     L.append("static constexpr uint32_t kCrcS4[4][256] = {" + ", ".join(
         "{" + ", ".join(f"0x{v:08x}u" for v in S) + "}" for S in S4) + "};")
+    lts = [0, 1, 0, 0, 1, 1, 0, 1, 0, 1, 0, 0, 0, 0, 0, 1, 1, 0, 0, 1, 0, 1, 0, 1, 1, 1, 1, 0, 0, 0, 0, 0,
+           0, 0, 0, 0, 0, 0, 1, 1, 0, 0, 1, 1, 0, 1, 0, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, 0, 1, 0, 1, 1, 1, 1]
+    L.append("// lts11a (OFDM/LTS.blk:45-49) as a bit mask: bit b set = LTS bin b is +1")
+    L.append(f"static constexpr uint64_t kLts11aBits = 0x{sum(v << b for b, v in enumerate(lts)):016x}ull;")
     L.append("// pilotSgn (PilotTrack.blk:70-78): bit m of kPilotNeg = entry m is -1")
     L.append("static constexpr uint32_t kPilotNeg[4] = {" + ", ".join(f"0x{v:08x}u" for v in pilot_neg_bits()) + "};")
     return "\n".join(L) + "\n"

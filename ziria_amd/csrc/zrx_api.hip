@@ -54,6 +54,13 @@ struct zrx_ctx {
   // ChannelEqualization / PilotTrack trig tables (built on first use)
   uint32_t* eq_rot = nullptr;     // 65536 x (cos, -sin) complex16
   int16_t* eq_atan = nullptr;     // 256 x 256 atan2x_lut
+  // RX front end (zrx_rx_stream_dev): STS pattern and per-capture staging, grown on demand
+  uint32_t* fe_pattern = nullptr; // 16 x 16 complex16
+  int fe_cap = 0, fe_sym = 0;     // captures x symbols per capture the staging holds
+  uint32_t* fe_syms = nullptr;
+  int64_t* fe_sym_off = nullptr;
+  int32_t* fe_nsym = nullptr;
+  uint32_t* fe_chan = nullptr;
   // per-call externals
   VitStream* vstream = nullptr;
   void* small = nullptr;          // staging for single calls
@@ -104,6 +111,87 @@ static void make_trig_tables(int16_t* sinv, int16_t* cosv, int16_t* atanv) {
   for (int i = 0; i < 256; i++)
     for (int j = 0; j < 256; j++)
       atanv[(i << 8) | j] = (int16_t)std::trunc(std::atan2((double)(int8_t)i, (double)(int8_t)j) / pi * 32768.0);
+}
+
+// ---- RX front end host tables -------------------------------------------------------
+// IFFT<64> (csrc/ifft_r4difx.hpp:56-250) for createSTSinTime (cca_tufv.blk:50-77); host
+// code, run once per context.  Saturating int16 (adds/subs), XOR-as-negate, conj_mul_shiftx
+// (csrc/sora_ext_lib_fft.hpp:68-94) with 32-bit madd wrap, 6-bit bit-reversed output.
+namespace hostfft {
+struct c16 { int16_t re, im; };
+static inline int16_t sat(int32_t x) { return (int16_t)std::min(32767, std::max(-32768, x)); }
+static inline int16_t inv(int16_t x) { return (int16_t)~x; }
+static inline c16 add(c16 a, c16 b) { return {sat(a.re + b.re), sat(a.im + b.im)}; }
+static inline c16 sub(c16 a, c16 b) { return {sat(a.re - b.re), sat(a.im - b.im)}; }
+static inline c16 shr2(c16 a) { return {(int16_t)(a.re >> 2), (int16_t)(a.im >> 2)}; }
+static inline c16 cmul(c16 a, int16_t br, int16_t bi) {
+  const int32_t re = (int32_t)((uint32_t)(a.re * br) + (uint32_t)(a.im * bi));
+  const int32_t im = (int32_t)((uint32_t)(a.im * br) + (uint32_t)(inv(a.re) * bi));
+  return {(int16_t)(re >> 15), (int16_t)(im >> 15)};
+}
+static void stage(c16* x, int N) {
+  const int16_t* t1 = N == 64 ? kTw64_1 : kTw16_1;
+  const int16_t* t2 = N == 64 ? kTw64_2 : kTw16_2;
+  const int16_t* t3 = N == 64 ? kTw64_3 : kTw16_3;
+  for (int n = 0; n < N / 4; n++) {
+    const c16 a = shr2(x[n]), b = shr2(x[n + N / 4]), c = shr2(x[n + N / 2]), d = shr2(x[n + 3 * N / 4]);
+    const c16 ac = add(a, c), bd = add(b, d), a_c = sub(a, c), b_d = sub(b, d);
+    x[n] = add(ac, bd);
+    x[n + N / 4] = cmul(sub(ac, bd), t2[2 * n], t2[2 * n + 1]);
+    const c16 jb = {inv(b_d.im), b_d.re};
+    x[n + N / 2] = cmul(add(a_c, jb), t1[2 * n], t1[2 * n + 1]);
+    x[n + 3 * N / 4] = cmul(sub(a_c, jb), t3[2 * n], t3[2 * n + 1]);
+  }
+}
+static void four(c16* x) {      // IFFTSSEEx<4> (:114-150)
+  const c16 y0 = shr2(x[0]), y1 = shr2(x[1]), y2 = shr2(x[2]), y3 = shr2(x[3]);
+  const c16 A = add(y0, y2), B = add(y1, y3);
+  const c16 C = add(y0, {inv(y2.re), inv(y2.im)}), D = add(y1, {inv(y3.re), inv(y3.im)});
+  const c16 jD = {inv(D.im), D.re};
+  x[0] = add(A, B);
+  x[1] = add({inv(B.re), inv(B.im)}, A);
+  x[2] = add(C, jD);
+  x[3] = add({inv(jD.re), inv(jD.im)}, C);
+}
+static void ifft64(const c16* in, c16* out) {
+  c16 x[64];
+  std::memcpy(x, in, sizeof(x));
+  stage(x, 64);
+  for (int q = 0; q < 4; q++) {
+    stage(x + 16 * q, 16);
+    for (int r = 0; r < 4; r++) four(x + 16 * q + 4 * r);
+  }
+  for (int i = 0; i < 64; i++) out[i] = x[bitrev6(i)];
+}
+}  // namespace hostfft
+
+// InitCorrPattern (cca_tufv.blk:80-98): pattern[16 i + j] = (sts_time[i + j] >> 7)
+static void make_cca_pattern(uint32_t* pattern) {
+  const int16_t m = (int16_t)(10720.0 * 1.472);      // int16(double(bpsk_mod_11a) * 1.472)
+  hostfft::c16 sts[64] = {}, t[64];
+  const int pos[12] = {4, 8, 12, 16, 20, 24, 40, 44, 48, 52, 56, 60};
+  const int sgn[12] = {-1, -1, 1, 1, 1, 1, 1, -1, 1, -1, -1, 1};
+  for (int i = 0; i < 12; i++) sts[pos[i]] = {(int16_t)(sgn[i] * m), (int16_t)(sgn[i] * m)};
+  hostfft::ifft64(sts, t);
+  for (int i = 0; i < 16; i++)
+    for (int j = 0; j < 16; j++) {
+      const hostfft::c16 v = t[i + j];
+      pattern[16 * i + j] = (uint32_t)(uint16_t)(v.re >> 7) | ((uint32_t)(uint16_t)(v.im >> 7) << 16);
+    }
+}
+
+// amp values where log2(1000 / sqrt(amp)) is an exact k + 0.5 (amp = 10^6 / 2^(2k+1)):
+// their rounding follows this host libm, like the reference's round_int32(log2(...)).
+static fe::AgcTies make_agc_ties() {
+  fe::AgcTies t;
+  for (int i = 0; i < 8; i++) {
+    const int k = 2 - i;                              // k = 2 .. -5
+    const double amp = 1e6 / std::ldexp(1.0, 2 * k + 1);
+    t.amp[i] = (int32_t)amp;
+    const double d = std::log(1000.0 / std::sqrt((double)t.amp[i])) / std::log(2.0);
+    t.agc[i] = (int32_t)((d > 0) ? (d + 0.5) : (d - 0.5));
+  }
+  return t;
 }
 
 static int ensure_eq_tables(zrx_ctx* c) {
@@ -174,6 +262,8 @@ int zrx_destroy(zrx_ctx* c) {
   free_ws(c);
   (void)hipFree(c->eq_rot);
   (void)hipFree(c->eq_atan);
+  for (void* p : {(void*)c->fe_pattern, (void*)c->fe_syms, (void*)c->fe_sym_off, (void*)c->fe_nsym, (void*)c->fe_chan})
+    (void)hipFree(p);
   (void)hipFree(c->vstream);
   (void)hipFree(c->small);
   for (auto& set : c->evsets)
@@ -324,6 +414,55 @@ int zrx_ofdm_eq_dev(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
                                                      (const uint32_t*)d_chan, EqTabs{c->eq_rot, c->eq_atan},
                                                      (uint4*)d_out);
   ZRX_CHECK(hipGetLastError());
+  return ZRX_OK;
+}
+
+int zrx_rx_stream_dev(zrx_ctx* c, const struct complex16* d_samples, const int64_t* d_cap_off,
+                      const int32_t* d_cap_len, int ncap, int max_len, int downsample, uint8_t* d_payload,
+                      int32_t* d_info, int32_t* d_det) {
+  if (!c || ncap < 0 || max_len < 0 || (ncap > 0 && (!d_samples || !d_cap_off || !d_cap_len || !d_payload ||
+                                                     !d_info || !d_det)))
+    return ZRX_EINVAL;
+  if (ncap == 0) return ZRX_OK;
+  const int n_max = downsample ? max_len / 8 * 4 : max_len;
+  const int max_sym = std::max(1, n_max / 80);       // symbols after the LTS fit in the capture
+  int rc = zrx_reserve(c, ncap, max_sym);
+  if (rc) return rc;
+  rc = ensure_eq_tables(c);
+  if (rc) return rc;
+  ZRX_CHECK(hipSetDevice(c->device));
+  if (!c->fe_pattern) {
+    uint32_t pat[256];
+    make_cca_pattern(pat);
+    ZRX_CHECK(hipMalloc(&c->fe_pattern, sizeof(pat)));
+    ZRX_CHECK(hipMemcpy(c->fe_pattern, pat, sizeof(pat), hipMemcpyHostToDevice));
+  }
+  if (ncap > c->fe_cap || max_sym > c->fe_sym) {
+    for (void* p : {(void*)c->fe_syms, (void*)c->fe_sym_off, (void*)c->fe_nsym, (void*)c->fe_chan}) (void)hipFree(p);
+    const int nc = std::max(ncap, c->fe_cap), ns = std::max(max_sym, c->fe_sym);
+    ZRX_CHECK(hipMalloc(&c->fe_syms, (size_t)nc * ns * 256 + 256));
+    ZRX_CHECK(hipMalloc(&c->fe_sym_off, (size_t)nc * 8 + 8));
+    ZRX_CHECK(hipMalloc(&c->fe_nsym, (size_t)nc * 4 + 4));
+    ZRX_CHECK(hipMalloc(&c->fe_chan, (size_t)nc * 256 + 256));
+    c->fe_cap = nc; c->fe_sym = ns;
+  }
+  const uint32_t* smp = (const uint32_t*)d_samples;
+  hipStream_t s = c->stream;
+  fe::k_fe_detect<<<blocks(ncap, 4), 256, 0, s>>>(smp, d_cap_off, d_cap_len, ncap, downsample, 1000, c->fe_pattern, d_det);
+  fe::k_fe_lts<<<blocks(ncap, 64), 64, 0, s>>>(smp, d_cap_off, d_cap_len, ncap, downsample, d_det, make_agc_ties(),
+                                              c->fe_chan);
+  fe::k_fe_gather<<<blocks(ncap, 4), 256, 0, s>>>(smp, d_cap_off, d_cap_len, ncap, downsample, d_det, max_sym,
+                                                  c->fe_syms, c->fe_sym_off, c->fe_nsym);
+  ZRX_CHECK(hipGetLastError());
+  return rx_chain(c, (const complex16*)c->fe_syms, c->fe_sym_off, c->fe_nsym, ncap, max_sym,
+                  (const complex16*)c->fe_chan, d_payload, d_info);
+}
+
+int zrx_cca_pattern(int16_t* pattern512) {
+  if (!pattern512) return ZRX_EINVAL;
+  uint32_t p[256];
+  make_cca_pattern(p);
+  std::memcpy(pattern512, p, sizeof(p));
   return ZRX_OK;
 }
 
@@ -589,6 +728,52 @@ int32_t __ext_wifi_rx_eq_batch(struct complex16* sym, int nsym_total, int32_t* p
   const int np = n_off - 1;
   if (np < 0 || !chan || chan_len < 64 * np) return ZRX_EINVAL;
   return wifi_rx_batch_impl(sym, nsym_total, pkt_sym_off, n_off, chan, payload, payload_len_bits, pkt_info, n_info);
+}
+
+int32_t __ext_wifi_rx_stream_batch(struct complex16* samples, int nsamples, int32_t* cap_off, int n_off,
+                                   int downsample, unsigned char* payload, int payload_len_bits,
+                                   int32_t* pkt_info, int n_info, int32_t* det, int n_det) {
+  const int nc = n_off - 1;
+  if (nc < 0 || nsamples < 0 || n_info < 8 * nc || n_det < fe::kDetWords * nc ||
+      (int64_t)payload_len_bits / 8 < (int64_t)nc * kPayloadStride)
+    return ZRX_EINVAL;
+  if (nc == 0) return 0;
+  std::vector<int64_t> off(nc);
+  std::vector<int32_t> len(nc);
+  int max_len = 0;
+  for (int i = 0; i < nc; i++) {
+    if (cap_off[i] < 0 || cap_off[i + 1] < cap_off[i] || cap_off[i + 1] > nsamples) return ZRX_EINVAL;
+    off[i] = cap_off[i];
+    len[i] = cap_off[i + 1] - cap_off[i];
+    max_len = std::max(max_len, len[i]);
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  zrx_ctx* c = default_ctx();
+  const size_t s_smp = ((size_t)nsamples * 4 + 255) / 256 * 256 + 256;
+  const size_t s_off = ((size_t)nc * 8 + 255) / 256 * 256, s_len = ((size_t)nc * 4 + 255) / 256 * 256;
+  const size_t s_pay = (size_t)nc * kPayloadStride, s_info = ((size_t)nc * 32 + 255) / 256 * 256;
+  const size_t s_det = (size_t)nc * 4 * fe::kDetWords;
+  uint8_t* d = (uint8_t*)staging(c, s_smp + s_off + s_len + s_pay + s_info + s_det + 1024);
+  if (!d) return ZRX_ENOMEM;
+  uint8_t* d_smp = d;
+  int64_t* d_off = (int64_t*)(d + s_smp);
+  int32_t* d_len = (int32_t*)((uint8_t*)d_off + s_off);
+  uint8_t* d_pay = (uint8_t*)d_len + s_len;
+  int32_t* d_info = (int32_t*)(d_pay + s_pay);
+  int32_t* d_det = (int32_t*)((uint8_t*)d_info + s_info);
+  ZRX_CHECK(hipMemcpyAsync(d_smp, samples, (size_t)nsamples * 4, hipMemcpyHostToDevice, c->stream));
+  ZRX_CHECK(hipMemcpyAsync(d_off, off.data(), (size_t)nc * 8, hipMemcpyHostToDevice, c->stream));
+  ZRX_CHECK(hipMemcpyAsync(d_len, len.data(), (size_t)nc * 4, hipMemcpyHostToDevice, c->stream));
+  ZRX_CHECK(hipMemsetAsync(d_pay, 0, s_pay, c->stream));
+  int rc = zrx_rx_stream_dev(c, (const complex16*)d_smp, d_off, d_len, nc, max_len, downsample, d_pay, d_info, d_det);
+  if (rc) return rc;
+  ZRX_CHECK(hipMemcpyAsync(payload, d_pay, s_pay, hipMemcpyDeviceToHost, c->stream));
+  ZRX_CHECK(hipMemcpyAsync(pkt_info, d_info, (size_t)nc * 32, hipMemcpyDeviceToHost, c->stream));
+  ZRX_CHECK(hipMemcpyAsync(det, d_det, s_det, hipMemcpyDeviceToHost, c->stream));
+  ZRX_CHECK(hipStreamSynchronize(c->stream));
+  int ok = 0;
+  for (int i = 0; i < nc; i++) ok += det[fe::kDetWords * i] && pkt_info[8 * i + 4] != 0;
+  return ok;
 }
 
 }  // extern "C"

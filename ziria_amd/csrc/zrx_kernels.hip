@@ -20,6 +20,7 @@
 #include "zrx_device.hpp"
 #include "zrx_viterbi2.hpp"
 #include "zrx_viterbi3.hpp"
+#include "zrx_frontend.hpp"
 
 namespace zrx {
 

@@ -108,3 +108,20 @@ class RxEngine:
         check(lib().zrx_ofdm_eq_dev(self._h, _ptr(sym), _ptr(sym_off), _ptr(nsym), n, _ptr(chan), _ptr(out)),
               "zrx_ofdm_eq_dev")
         return out
+
+    def rx_stream(self, samples, cap_off, cap_len, max_len, downsample=False, payload=None, info=None, det=None):
+        """receiver() (receiver.blk:57-72) once per capture: samples int16 [S, 2] on the device,
+        cap_off int64 / cap_len int32 [n] in samples.  Returns (payload uint8 [n,4096], info
+        int32 [n,8], det int32 [n,8] = {detected, noSamples, shift, energy, noise, maxCorr,
+        consumed, data_start})."""
+        n = cap_off.numel()
+        assert samples.dtype == torch.int16 and cap_off.dtype == torch.int64 and cap_len.dtype == torch.int32
+        dev = samples.device
+        payload = torch.zeros((n, PAYLOAD_STRIDE), dtype=torch.uint8, device=dev) if payload is None else payload
+        info = torch.zeros((n, 8), dtype=torch.int32, device=dev) if info is None else info
+        det = torch.zeros((n, 8), dtype=torch.int32, device=dev) if det is None else det
+        self._stream()
+        check(lib().zrx_rx_stream_dev(self._h, _ptr(samples), _ptr(cap_off), _ptr(cap_len), n, int(max_len),
+                                      1 if downsample else 0, _ptr(payload), _ptr(info), _ptr(det)),
+              "zrx_rx_stream_dev")
+        return payload, info, det

@@ -142,3 +142,20 @@ def wifi_rx_eq_batch(sym, pkt_sym_off, chan):
     if rc < 0:
         raise ZiriaRxError(f"__ext_wifi_rx_eq_batch failed ({rc})")
     return pay[:n], {k: info[:n, i].copy() for i, k in enumerate(INFO_FIELDS)}, int(rc)
+
+
+def wifi_rx_stream_batch(samples, cap_off, downsample=False):
+    """receiver() once per capture (receiver.blk:57-72) over host arrays: samples int16
+    [S, 2]; cap_off (n+1) CSR sample offsets.  Returns (payload uint8 [n, 4096], info dict,
+    det int32 [n, 8], count of detected packets whose CRC passed)."""
+    x = np.ascontiguousarray(samples, dtype=np.int16).reshape(-1, 2)
+    off = np.ascontiguousarray(cap_off, np.int32)
+    n = off.size - 1
+    pay = np.zeros((max(n, 1), PAYLOAD_STRIDE), np.uint8)
+    info = np.zeros((max(n, 1), 8), np.int32)
+    det = np.zeros((max(n, 1), 8), np.int32)
+    rc = lib().__ext_wifi_rx_stream_batch(_p(x), x.shape[0], _p(off), off.size, 1 if downsample else 0,
+                                          _p(pay), pay.size * 8, _p(info), info.size, _p(det), det.size)
+    if rc < 0:
+        raise ZiriaRxError(f"__ext_wifi_rx_stream_batch failed ({rc})")
+    return pay[:n], {k: info[:n, i].copy() for i, k in enumerate(INFO_FIELDS)}, det[:n], int(rc)
