@@ -63,10 +63,12 @@ def main():
     ap.add_argument("--payload", type=int, default=1500)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall time budget of the CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 5])
+    ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 5])
     ap.add_argument("--eq", action="store_true",
                     help="config 3 through a channel, with ChannelEqualization + PilotTrack (SURVEY §8f row 1)")
     args = ap.parse_args()
+    if args.config == 1:
+        return bench_capture(args)
     if args.config == 2:
         return bench_viterbi_only(args)
     if args.config == 5:
@@ -282,6 +284,69 @@ def bench_mixed(args):
         "cpu_baseline": {"value": round(cpu_bits / cpu_dt / 1e6, 2), "unit": "Mbit/s",
                          "cores": min(16, os.cpu_count() or 1), "kind": "port",
                          "sample": f"first {sample} packets, {cpu_dt:.2f} s"},
+    }), flush=True)
+
+
+def bench_capture(args):
+    """BASELINE config 1: the recorded over-the-air packet of code/WiFi/tests/test_real_rx
+    (committed as data in tests/golden/ref_fe.npz) through receiver() -- removeDC, CCA,
+    LTS, DataSymbol, FFT, ChannelEqualization, PilotTrack, decode -- batched over captures:
+    capture 0 is the KAT stream itself (checked against its ground output), the others the
+    same recording with fresh noise, gains and idle lengths."""
+    import numpy as np
+    from oracle import oracle as O
+    from tests import fe_cases
+    dev = torch.device("cuda", 0)
+    fe = np.load(os.path.join(ROOT, "tests", "golden", "ref_fe.npz"))
+    n = args.npkts if args.npkts != 16384 else 4096
+    rng = np.random.default_rng(0xC0F1)
+    _, real = fe_cases.kat_streams(fe)
+    caps = [real]
+    for i in range(1, n):
+        g = rng.uniform(0.7, 1.5)
+        idle = int(rng.integers(340, 1000))
+        sig = np.concatenate([np.zeros((idle, 2)), real[1000:].astype(np.float64) * g])
+        sig += rng.normal(0, 1.0, sig.shape)
+        caps.append(np.clip(np.rint(sig), -32768, 32767).astype(np.int16))
+    off = np.cumsum([0] + [c.shape[0] for c in caps]).astype(np.int64)
+    x = torch.from_numpy(np.concatenate(caps)).to(dev)
+    coff = torch.from_numpy(off[:-1]).to(dev)
+    clen = torch.from_numpy(np.diff(off).astype(np.int32)).to(dev)
+    max_len = int(np.diff(off).max())
+    eng = RxEngine(0)
+    payload = torch.zeros((n, 4096), dtype=torch.uint8, device=dev)
+    info = torch.zeros((n, 8), dtype=torch.int32, device=dev)
+    det = torch.zeros((n, 8), dtype=torch.int32, device=dev)
+    step = lambda: eng.rx_stream(x, coff, clen, max_len, False, payload, info, det)
+    elapsed = _timed(step, args.steps, args.warmup)
+    inf, pay, dt = info.cpu().numpy(), payload.cpu().numpy(), det.cpu().numpy()
+    ok = (inf[:, 4] == 1) & (dt[:, 0] == 1)
+    bits = int(((inf[:, 2] - 4) * 8 * ok).sum())
+    kat = fe["real_out"]
+    kat_ok = bool(ok[0] and (pay[0, :kat.size] == kat).all())
+    sample = min(64, n)
+    t0 = time.perf_counter()
+    cpu_ok = cpu_bits = 0
+    match = True
+    for i in range(sample):
+        opay, r, odet, _, _ = O.rx_stream(caps[i])
+        if r["ret"] == 0 and r["crc_ok"]:
+            cpu_ok += 1
+            cpu_bits += (r["len"] - 4) * 8
+            match &= bool((pay[i, :r["len"] - 4] == opay).all())
+    cpu_dt = time.perf_counter() - t0
+    print(json.dumps({
+        "metric": "decoded Mbit/s, recorded 802.11a packet through the full receiver (BASELINE config 1)",
+        "value": round(bits * args.steps / elapsed / 1e6, 2), "unit": "Mbit/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int16+int32",
+        "data": "recorded capture (test_real_rx.infile) + noise/gain/idle variants",
+        "config": {"workload": f"config1: {n} captures of {max_len} samples max, receiver() per capture",
+                   "captures_per_s": round(n * args.steps / elapsed, 1)},
+        "bit_exact_check": {"kat_capture_matches_ground": kat_ok, "crc_pass": int(ok.sum()),
+                            "oracle_sample_match": match, "oracle_sample_crc_pass": cpu_ok},
+        "cpu_baseline": {"value": round(cpu_bits / cpu_dt / 1e6, 3), "unit": "Mbit/s", "cores": 1,
+                         "kind": "port", "sample": f"first {sample} captures, {cpu_dt:.2f} s"},
     }), flush=True)
 
 
