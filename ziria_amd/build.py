@@ -21,8 +21,27 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
+DRIVER = os.path.join(LIBDIR, "ziria_rx_driver")
+DRIVER_SRC = os.path.join(HERE, "..", "tools", "ziria_rx_driver.cpp")
+
+
+def build_driver(verbose=False):
+    """The batching driver (tools/ziria_rx_driver.cpp), a host program linked against the
+    library (rpath $ORIGIN, next to it in ziria_amd/_lib)."""
+    if os.path.exists(DRIVER) and os.path.getmtime(DRIVER) >= max(os.path.getmtime(DRIVER_SRC), os.path.getmtime(LIB)):
+        return DRIVER
+    cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-o", DRIVER + ".tmp", DRIVER_SRC, "-L" + LIBDIR, "-lziria_rx",
+           "-Wl,-rpath,$ORIGIN"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    os.replace(DRIVER + ".tmp", DRIVER)
+    return DRIVER
+
+
 def build(force=False, verbose=False):
     if not force and not _stale():
+        build_driver(verbose)
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
     subprocess.check_call([sys.executable, os.path.join(CSRC, "gen_tables.py")])
@@ -32,6 +51,7 @@ def build(force=False, verbose=False):
         print(" ".join(cmd))
     subprocess.check_call(cmd, cwd=CSRC)
     os.replace(LIB + ".tmp", LIB)
+    build_driver(verbose)
     return LIB
 
 
