@@ -109,6 +109,15 @@ int32_t __ext_wifi_rx_stream_batch(struct complex16* samples, int nsamples, int3
                                    int downsample, unsigned char* payload, int payload_len_bits,
                                    int32_t* pkt_info, int n_info, int32_t* det, int n_det);
 
+/* transmitter() of code/WiFi/transmitter/transmitter.blk:128-133 per packet, at its default
+ * 40 MHz oversampling (128-point IFFT, 32-sample cyclic prefix): packet i = in[pkt_in_off[i]
+ * .. pkt_in_off[i+1]) = 3 PLCP header bytes (emitHeader: RATE, LENGTH, parity, tail as the
+ * air bits) then LENGTH-4 payload bytes.  Writes 640 preamble samples + 160 per OFDM symbol
+ * (SIGNAL + data) at out[pkt_out_off[i] ..] (n_oo >= npkts+1 offsets filled by the call).
+ * Returns the total number of complex16 samples written, or a negative ZRX_E* code. */
+int32_t __ext_wifi_tx_batch(unsigned char* in, int inlen, int32_t* pkt_in_off, int n_off,
+                            struct complex16* out, int outlen, int32_t* pkt_out_off, int n_oo);
+
 /* ================================================================ Part 3: device API */
 
 #define ZRX_OK 0
@@ -176,6 +185,16 @@ int zrx_ofdm_eq_dev(zrx_ctx* ctx, const struct complex16* d_sym, const int64_t* 
 int zrx_rx_stream_dev(zrx_ctx* ctx, const struct complex16* d_samples, const int64_t* d_cap_off,
                       const int32_t* d_cap_len, int ncap, int max_len, int downsample,
                       uint8_t* d_payload, int32_t* d_info, int32_t* d_det);
+
+/* transmitter() per packet on device buffers (as __ext_wifi_tx_batch): d_in_off int64 byte
+ * offsets, d_out_off int64 sample offsets with room for zrx_tx_samples(header) samples,
+ * d_nsamp receives each packet's sample count. */
+int zrx_tx_dev(zrx_ctx* ctx, const uint8_t* d_in, const int64_t* d_in_off, int npkts,
+               struct complex16* d_out, const int64_t* d_out_off, int32_t* d_nsamp);
+/* Samples transmitter() emits for a packet with these 3 PLCP header bytes (host, no GPU). */
+int zrx_tx_samples(const uint8_t* hdr3);
+/* Host-side copy of the 640-sample 40 MHz preamble (createPreamble.blk). */
+int zrx_tx_preamble(int16_t* out1280);
 
 /* Host-side copy of the STS correlation pattern of cca (cca_tufv.blk:80-98), 16 x 16
  * complex16.  No GPU needed. */

@@ -377,3 +377,36 @@ def rx_stream(x):
     d["ret"] = ret
     dd = {k: getattr(det, k) for k, _ in CCA._fields_}
     return pay[: max(d["len"] - 4, 0)].copy(), d, dd, co, d0.value
+
+
+
+# ---------------------------------------------------------------- TX chain
+def ifft128(x):
+    x = np.ascontiguousarray(x, np.int16).reshape(128, 2)
+    o = np.zeros_like(x)
+    lib().zo_ifft128(_p(x), _p(o))
+    return o
+
+
+def tx_preamble():
+    o = np.zeros((640, 2), np.int16)
+    lib().zo_tx_preamble(_p(o))
+    return o
+
+
+def tx_packet(inp):
+    """transmitter() on one packet: 3 PLCP header bytes + payload -> int16 [n, 2] samples."""
+    inp = np.ascontiguousarray(inp, np.uint8)
+    out = np.zeros((640 + 160 * 1500, 2), np.int16)
+    n = lib().zo_tx_packet(_p(inp), inp.size, _p(out), out.shape[0])
+    assert n > 0, n
+    return out[:n].copy()
+
+
+def plcp_header(mod, coding, length):
+    """The 3 air bytes of a PLCP header (RATE, LENGTH, parity, tail; parsePLCPHeader.blk)."""
+    rate = {(0, 0): 0xB, (0, 2): 0xF, (1, 0): 0xA, (1, 2): 0xE, (2, 0): 0x9, (2, 2): 0xD,
+            (3, 1): 0x8, (3, 2): 0xC}[(mod, coding)]
+    h = rate | (length << 5)
+    h |= (bin(h).count("1") & 1) << 17
+    return np.array([h & 255, (h >> 8) & 255, (h >> 16) & 255], np.uint8)

@@ -26,3 +26,5 @@ void zref_v_mul_complex16(struct complex16* out, struct complex16* x, struct com
 // IFFT<64> brick (csrc/sora_ext_lib.cpp:2828), for the STS pattern of cca_tufv.blk
 extern "C" __attribute__((visibility("default")))
 void zref_sora_ifft64(struct complex16* out, struct complex16* in) { __ext_sora_ifft(out, 64, in, 64); }
+extern "C" __attribute__((visibility("default")))
+void zref_sora_ifft128(struct complex16* out, struct complex16* in) { __ext_sora_ifft(out, 128, in, 128); }

@@ -588,6 +588,15 @@ int zo_tx_signal_symbol(int mod, int coding, int len, zo_c16* sub48) {
   interleave_map(0, coded, sub48);
   return 1;
 }
+/* SIGNAL symbol from the 24 header bits as given (emitHeader, parsePLCPHeader.blk:215-221):
+   encode12 >>> interleaver_bpsk >>> modulate_bpsk */
+int zo_tx_signal_from_bits(const uint8_t* hbits3, zo_c16* sub48) {
+  uint8_t h[24], coded[48];
+  for (int k = 0; k < 24; k++) h[k] = (hbits3[k >> 3] >> (k & 7)) & 1;
+  zo_tx_encode(h, 24, 0, coded);
+  interleave_map(0, coded, sub48);
+  return 1;
+}
 /* tx_driver (transmitter.blk:56-101): crcXX(len,true) >>> scrambler(1011101) >>> encode >>>
    interleave >>> modulate.  Returns the number of data symbols. */
 int zo_tx_data_symbols(const uint8_t* payload, int plen, int mod, int coding, zo_c16* sub48, int max_sym) {

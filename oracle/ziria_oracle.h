@@ -128,6 +128,12 @@ int zo_tx_data_symbols(const uint8_t* payload, int len_minus4, int mod, int codi
                        zo_c16* sub48, int max_sym);
 int zo_tx_signal_symbol(int mod, int coding, int len, zo_c16* sub48);
 int zo_tx_encode(const uint8_t* bits, int nbits, int coding, uint8_t* coded);  /* encoding.blk */
+int zo_tx_signal_from_bits(const uint8_t* hbits3, zo_c16* sub48);              /* emitHeader >>> encode12 .. */
+/* TX chain at 40 MHz, ziria_oracle_fe.c */
+void zo_ifft128(const zo_c16* in, zo_c16* out);                    /* IFFT<128>, ifft_r4difx.hpp */
+void zo_tx_preamble(zo_c16* out640);                                /* createPreamble.blk */
+void zo_tx_symbol(const zo_c16* sub48, int k, zo_c16* out160);      /* map_ofdm >>> ifft */
+int  zo_tx_packet(const uint8_t* in, int nin, zo_c16* out, int max_out);   /* transmitter() */
 
 #ifdef __cplusplus
 }

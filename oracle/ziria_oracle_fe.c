@@ -336,3 +336,135 @@ int zo_rx_stream(const zo_c16* x, int n, uint8_t* payload, zo_rx_result* r, zo_c
   free(sym);
   return ret;
 }
+
+/* ---- TX chain: transmitter() of code/WiFi/transmitter/transmitter.blk:128-133
+   at the default 40 MHz oversampling (FFT_SIZE 128, CP_SIZE 32) ------------------------------ */
+/* IFFTSSEEx<8> (csrc/ifft_r4difx.hpp:152-228): a = x[0..3] >> 3, b = x[4..7] >> 3; the sum
+   half takes the 4-point combination of IFFTSSEEx<4> (no further shift), the difference half
+   e = a - b is rotated (j e2, j e3), combined, multiplied by conj(tw8) and combined again. */
+static void ifft8(zo_c16* x) {
+  zo_c16 a[4], b[4], s[4], e[4];
+  for (int k = 0; k < 4; k++) {
+    a[k].re = (int16_t)(x[k].re >> 3); a[k].im = (int16_t)(x[k].im >> 3);
+    b[k].re = (int16_t)(x[k + 4].re >> 3); b[k].im = (int16_t)(x[k + 4].im >> 3);
+    s[k] = cadd(a[k], b[k]);
+    e[k] = csub(a[k], b[k]);
+  }
+  const zo_c16 A = cadd(s[0], s[2]), B = cadd(s[1], s[3]);
+  const zo_c16 C = cadd((zo_c16){inv16(s[2].re), inv16(s[2].im)}, s[0]);
+  const zo_c16 D = cadd((zo_c16){inv16(s[3].re), inv16(s[3].im)}, s[1]);
+  const zo_c16 jD = {inv16(D.im), D.re};
+  zo_c16 o[8];
+  o[0] = cadd(A, B);
+  o[1] = cadd((zo_c16){inv16(B.re), inv16(B.im)}, A);
+  o[2] = cadd(C, jD);
+  o[3] = cadd((zo_c16){inv16(jD.re), inv16(jD.im)}, C);
+  const zo_c16 je2 = {inv16(e[2].im), e[2].re}, je3 = {inv16(e[3].im), e[3].re};
+  zo_c16 t[4];
+  t[0] = cadd(e[0], je2);
+  t[1] = cadd(e[1], je3);
+  t[2] = cadd((zo_c16){inv16(je2.re), inv16(je2.im)}, e[0]);
+  t[3] = cadd((zo_c16){inv16(je3.re), inv16(je3.im)}, e[1]);
+  static const int16_t tw[4][2] = {{32767, 0}, {23169, -23169}, {32767, 0}, {-23169, -23169}};
+  zo_c16 u[4];
+  for (int k = 0; k < 4; k++) u[k] = conj_mul_shift(t[k], tw[k][0], tw[k][1]);
+  o[4] = cadd(u[0], u[1]);
+  o[5] = cadd((zo_c16){inv16(u[1].re), inv16(u[1].im)}, u[0]);
+  o[6] = cadd(u[2], u[3]);
+  o[7] = cadd((zo_c16){inv16(u[3].re), inv16(u[3].im)}, u[2]);
+  memcpy(x, o, sizeof(o));
+}
+static int bitrev7(int i) {
+  int r = 0;
+  for (int b = 0; b < 7; b++) r |= ((i >> b) & 1) << (6 - b);
+  return r;
+}
+/* IFFT<128>: IFFTSSE<128>, then per quarter IFFTSSE<32> and IFFTSSEEx<8> x 4; output
+   through FFT128LUTMap (csrc/fft_lut_bitreversal.h:153), the 7-bit bit reversal */
+void zo_ifft128(const zo_c16* in, zo_c16* out) {
+  zo_c16 x[128];
+  memcpy(x, in, sizeof(x));
+  ifft_stage(x, 128);
+  for (int q = 0; q < 4; q++) {
+    ifft_stage(x + 32 * q, 32);
+    for (int r = 0; r < 4; r++) ifft8(x + 32 * q + 8 * r);
+  }
+  for (int i = 0; i < 128; i++) out[i] = x[bitrev7(i)];
+}
+
+/* createSTSinTime / createLTSinTime (createPreamble.blk:38-117), 320 samples each */
+void zo_tx_preamble(zo_c16* out640) {
+  const int16_t sm = (int16_t)(10720.0 * 1.472), lm = 10720;
+  zo_c16 f[128], t[128];
+  memset(f, 0, sizeof(f));
+  const int sp[12] = {4, 8, 12, 16, 20, 24, 104, 108, 112, 116, 120, 124};
+  const int ss[12] = {-1, -1, 1, 1, 1, 1, 1, -1, 1, -1, -1, 1};
+  for (int i = 0; i < 12; i++) { f[sp[i]].re = (int16_t)(ss[i] * sm); f[sp[i]].im = (int16_t)(ss[i] * sm); }
+  zo_ifft128(f, t);
+  memcpy(out640, t, sizeof(t));
+  memcpy(out640 + 128, t, sizeof(t));
+  memcpy(out640 + 256, t, 64 * sizeof(zo_c16));
+  static const uint8_t pos[64] = {0, 1, 0, 0, 1, 1, 0, 1, 0, 1, 0, 0, 0, 0, 0, 1, 1, 0, 0, 1, 0, 1, 0, 1, 1, 1, 1, 0, 0, 0, 0, 0,
+                                  0, 0, 0, 0, 0, 0, 1, 1, 0, 0, 1, 1, 0, 1, 0, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, 0, 1, 0, 1, 1, 1, 1};
+  memset(f, 0, sizeof(f));
+  for (int i = 1; i <= 26; i++) f[i].re = pos[i] ? lm : (int16_t)-lm;
+  for (int i = 38; i < 64; i++) f[i + 64].re = pos[i] ? lm : (int16_t)-lm;
+  zo_ifft128(f, t);
+  zo_c16* l = out640 + 320;
+  memcpy(l + 64, t, sizeof(t));
+  memcpy(l + 192, t, sizeof(t));
+  memcpy(l, l + 256, 64 * sizeof(zo_c16));
+}
+
+/* map_ofdm (map_ofdm.blk:63-107) + ifft (ifft.blk:35-52): 48 subcarriers (GetData order) and
+   the pilots of symbol k (allPilots index 127 for k = 0, then 0, 1, ...) -> 160 samples */
+void zo_tx_symbol(const zo_c16* sub48, int k, zo_c16* out160) {
+  const int idx = k == 0 ? 127 : (k - 1) % 127;
+  const int16_t B = 10720;
+  const int neg = zo_pilot_sign(idx) == -1;
+  const int16_t p = neg ? (int16_t)-B : B;
+  zo_c16 pil[4] = {{p, 0}, {(int16_t)-p, 0}, {p, 0}, {p, 0}};  /* allPilots, :40-49 */
+  zo_c16 e[64];
+  memset(e, 0, sizeof(e));
+  for (int i = 0; i < 48; i++) {
+    static const int bins[48] = {38, 39, 40, 41, 42, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56,
+                                 58, 59, 60, 61, 62, 63, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 13, 14, 15,
+                                 16, 17, 18, 19, 20, 22, 23, 24, 25, 26};
+    e[(bins[i] + 32) & 63] = sub48[i];           /* emitted index = carrier + 32 mod 64 */
+  }
+  e[(43 + 32) & 63] = pil[2];
+  e[(57 + 32) & 63] = pil[3];
+  e[(7 + 32) & 63] = pil[0];
+  e[(21 + 32) & 63] = pil[1];
+  zo_c16 sym[128], t[128];
+  memset(sym, 0, sizeof(sym));
+  memcpy(sym + 96, e, 32 * sizeof(zo_c16));
+  memcpy(sym, e + 32, 32 * sizeof(zo_c16));
+  zo_ifft128(sym, t);
+  memcpy(out160 + 32, t, sizeof(t));
+  memcpy(out160, t + 96, 32 * sizeof(zo_c16));
+}
+
+/* transmitter() on one packet: input = 3 PLCP header bytes (emitHeader) + len-4 payload bytes.
+   Writes 640 + 160 * (1 + nsym) samples to out (capacity max_out), returns their number. */
+int zo_tx_packet(const uint8_t* in, int nin, zo_c16* out, int max_out) {
+  if (nin < 3) return -1;
+  zo_hdr h;
+  uint8_t hb[4] = {in[0], in[1], in[2], 0};
+  zo_parse_header(hb, &h);
+  const int plen = h.len - 4;
+  if (plen < 0 || 3 + plen > nin) return -1;
+  const int nd = zo_ndbps(h.modulation, h.coding);
+  const int nsym = ((16 + plen * 8 + 32 + 6) + nd - 1) / nd;
+  const int total = 640 + 160 * (1 + nsym);
+  if (total > max_out) return -1;
+  zo_tx_preamble(out);
+  zo_c16 sub[48];
+  zo_tx_signal_from_bits(in, sub);
+  zo_tx_symbol(sub, 0, out + 640);
+  zo_c16* d = (zo_c16*)malloc(sizeof(zo_c16) * 48 * (size_t)nsym);
+  zo_tx_data_symbols(in + 3, plen, h.modulation, h.coding, d, nsym);
+  for (int k = 0; k < nsym; k++) zo_tx_symbol(d + 48 * k, k + 1, out + 640 + 160 * (1 + k));
+  free(d);
+  return total;
+}

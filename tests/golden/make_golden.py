@@ -281,6 +281,19 @@ def fe_vectors(R):
     for tag, name in (("rx", "test_rx"), ("real", "test_real_rx")):
         d[f"{tag}_in"] = rd(W + f"/tests/{name}.infile").reshape(-1, 2).astype(np.int16)
         d[f"{tag}_out"] = rd(W + f"/tests/{name}.outfile.ground").astype(np.int8).view(np.uint8)
+    d["tx_in"] = rd(W + "/tests/test_tx.infile").astype(np.int8).view(np.uint8)
+    d["tx_out"] = rd(W + "/tests/test_tx.outfile.ground").reshape(-1, 2).astype(np.int16)
+    x = np.zeros((40, 128, 2), np.int16)                 # IFFT<128> vectors (the TX's 40 MHz IFFT)
+    rng0 = np.random.default_rng(0x128)
+    x[:20] = rng0.integers(-32768, 32768, (20, 128, 2))
+    x[20:] = rng0.choice(np.array([-32768, 32767, 0, 10720, -10720], np.int16), (20, 128, 2))
+    o = np.zeros_like(x)
+    for i in range(40):
+        xi = np.ascontiguousarray(x[i])
+        oi = np.zeros_like(xi)
+        R.zref_sora_ifft128(ptr(oi), ptr(xi))
+        o[i] = oi
+    d["ifft128_in"], d["ifft128_out"] = x, o
     T = W + "/receiver/tests/"
     for tag, name in (("rdc", "test_c_RemoveDC"), ("ds", "test_c_DownSample"), ("dsym", "test_c_DataSymbol"),
                       ("lts", "test_c_LTS")):

@@ -32,6 +32,7 @@ SIGNATURES = [
     ("__ext_wifi_rx_eq_batch", C.c_int32, [_P, C.c_int, _P, C.c_int, _P, C.c_int, _P, C.c_int, _P, C.c_int]),
     ("__ext_wifi_rx_stream_batch", C.c_int32, [_P, C.c_int, _P, C.c_int, C.c_int, _P, C.c_int, _P, C.c_int, _P,
                                                C.c_int]),
+    ("__ext_wifi_tx_batch", C.c_int32, [_P, C.c_int, _P, C.c_int, _P, C.c_int, _P, C.c_int]),
     ("zrx_create", C.c_int, [C.POINTER(C.c_void_p), C.c_int, _P]),
     ("zrx_destroy", C.c_int, [_P]),
     ("zrx_set_stream", C.c_int, [_P, _P]),
@@ -45,6 +46,9 @@ SIGNATURES = [
     ("zrx_ofdm_eq_dev", C.c_int, [_P, _P, _P, _P, C.c_int, _P, _P]),
     ("zrx_rx_stream_dev", C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, C.c_int, _P, _P, _P]),
     ("zrx_cca_pattern", C.c_int, [_P]),
+    ("zrx_tx_dev", C.c_int, [_P, _P, _P, C.c_int, _P, _P, _P]),
+    ("zrx_tx_samples", C.c_int, [_P]),
+    ("zrx_tx_preamble", C.c_int, [_P]),
     ("zrx_trig_tables", C.c_int, [_P, _P, _P]),
     ("zrx_version", C.c_char_p, []),
 ]

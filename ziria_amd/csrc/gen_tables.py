@@ -146,7 +146,7 @@ def pilot_neg_bits():
 
 def render():
     L = ["// GENERATED by gen_tables.py — do not edit.", "#pragma once", "#include <stdint.h>", ""]
-    for N in (16, 64):
+    for N in (16, 32, 64, 128):
         for k in (1, 2, 3):
             vals = [twiddle(N, k, n) for n in range(N // 4)]
             L.append(f"// twFFTLUT{N}_{k} (csrc/sora_ext_lib_fft_coeffs.hpp), (re, im)")
@@ -164,6 +164,12 @@ def render():
         L.append(f"// Deinterleave (N_CBPS={N}): out[k] = in[kDeint{N}[k]]")
         L.append(f"static constexpr uint16_t kDeint{N}[{N}] = {{" +
                  ", ".join(str(deint_src(N, k)) for k in range(N)) + "};")
+    for N in (48, 96, 192, 288):
+        inv = [0] * N
+        for k in range(N):
+            inv[deint_src(N, k)] = k
+        L.append(f"// Interleave (N_CBPS={N}, interleaving.blk): interleaved bit j = coded bit kIntlv{N}[j]")
+        L.append(f"static constexpr uint16_t kIntlv{N}[{N}] = {{" + ", ".join(map(str, inv)) + "};")
     L.append("// reflected CRC-32 byte table (crc.blk:41-73, base32 = 0x04C11DB7)")
     L.append("static constexpr uint32_t kCrcTab[256] = {" + ", ".join(f"0x{v:08x}u" for v in crc_table()) + "};")
     L.append("// kCrcZero[k][i]: CRC register image of bit i after 2^k zero bytes")
@@ -190,6 +196,14 @@ def render():
            0, 0, 0, 0, 0, 0, 1, 1, 0, 0, 1, 1, 0, 1, 0, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, 0, 1, 0, 1, 1, 1, 1]
     L.append("// lts11a (OFDM/LTS.blk:45-49) as a bit mask: bit b set = LTS bin b is +1")
     L.append(f"static constexpr uint64_t kLts11aBits = 0x{sum(v << b for b, v in enumerate(lts)):016x}ull;")
+    st, key = [1, 0, 1, 1, 1, 0, 1], []
+    for _ in range(127):
+        t = st[3] ^ st[0]
+        st = st[1:] + [t]
+        key.append(t)
+    L.append("// TX scrambler keystream (scramble.blk:28-44, default_scrmbl_st = 1011101): bit m of kTxKey")
+    L.append("static constexpr uint32_t kTxKey[4] = {" + ", ".join(
+        f"0x{sum(key[32 * w + b] << b for b in range(32) if 32 * w + b < 127):08x}u" for w in range(4)) + "};")
     L.append("// pilotSgn (PilotTrack.blk:70-78): bit m of kPilotNeg = entry m is -1")
     L.append("static constexpr uint32_t kPilotNeg[4] = {" + ", ".join(f"0x{v:08x}u" for v in pilot_neg_bits()) + "};")
     return "\n".join(L) + "\n"

@@ -61,6 +61,7 @@ struct zrx_ctx {
   int64_t* fe_sym_off = nullptr;
   int32_t* fe_nsym = nullptr;
   uint32_t* fe_chan = nullptr;
+  uint32_t* tx_preamble = nullptr; // 640 complex16 (TX, createPreamble.blk)
   // per-call externals
   VitStream* vstream = nullptr;
   void* small = nullptr;          // staging for single calls
@@ -153,6 +154,48 @@ static void four(c16* x) {      // IFFTSSEEx<4> (:114-150)
   x[2] = add(C, jD);
   x[3] = add({inv(jD.re), inv(jD.im)}, C);
 }
+static void eight(c16* x) {     // IFFTSSEEx<8> (:152-228)
+  c16 sm[4], e[4];
+  for (int k = 0; k < 4; k++) {
+    const c16 a = {(int16_t)(x[k].re >> 3), (int16_t)(x[k].im >> 3)}, b = {(int16_t)(x[k + 4].re >> 3), (int16_t)(x[k + 4].im >> 3)};
+    sm[k] = add(a, b);
+    e[k] = sub(a, b);
+  }
+  const c16 A = add(sm[0], sm[2]), B = add(sm[1], sm[3]);
+  const c16 C = add({inv(sm[2].re), inv(sm[2].im)}, sm[0]), D = add({inv(sm[3].re), inv(sm[3].im)}, sm[1]);
+  const c16 jD = {inv(D.im), D.re};
+  c16 o[8];
+  o[0] = add(A, B); o[1] = add({inv(B.re), inv(B.im)}, A);
+  o[2] = add(C, jD); o[3] = add({inv(jD.re), inv(jD.im)}, C);
+  const c16 je2 = {inv(e[2].im), e[2].re}, je3 = {inv(e[3].im), e[3].re};
+  const c16 u0 = cmul(add(e[0], je2), 32767, 0), u1 = cmul(add(e[1], je3), 23169, -23169);
+  const c16 u2 = cmul(add({inv(je2.re), inv(je2.im)}, e[0]), 32767, 0);
+  const c16 u3 = cmul(add({inv(je3.re), inv(je3.im)}, e[1]), -23169, -23169);
+  o[4] = add(u0, u1); o[5] = add({inv(u1.re), inv(u1.im)}, u0);
+  o[6] = add(u2, u3); o[7] = add({inv(u3.re), inv(u3.im)}, u2);
+  std::memcpy(x, o, sizeof(o));
+}
+static void stage_n(c16* x, int N, const int16_t* t1, const int16_t* t2, const int16_t* t3) {
+  for (int n = 0; n < N / 4; n++) {
+    const c16 a = shr2(x[n]), b = shr2(x[n + N / 4]), c = shr2(x[n + N / 2]), d = shr2(x[n + 3 * N / 4]);
+    const c16 ac = add(a, c), bd = add(b, d), a_c = sub(a, c), b_d = sub(b, d);
+    x[n] = add(ac, bd);
+    x[n + N / 4] = cmul(sub(ac, bd), t2[2 * n], t2[2 * n + 1]);
+    const c16 jb = {inv(b_d.im), b_d.re};
+    x[n + N / 2] = cmul(add(a_c, jb), t1[2 * n], t1[2 * n + 1]);
+    x[n + 3 * N / 4] = cmul(sub(a_c, jb), t3[2 * n], t3[2 * n + 1]);
+  }
+}
+static void ifft128(const c16* in, c16* out) {
+  c16 x[128];
+  std::memcpy(x, in, sizeof(x));
+  stage_n(x, 128, kTw128_1, kTw128_2, kTw128_3);
+  for (int q = 0; q < 4; q++) {
+    stage_n(x + 32 * q, 32, kTw32_1, kTw32_2, kTw32_3);
+    for (int r = 0; r < 4; r++) eight(x + 32 * q + 8 * r);
+  }
+  for (int i = 0; i < 128; i++) out[i] = x[tx::bitrev7(i)];
+}
 static void ifft64(const c16* in, c16* out) {
   c16 x[64];
   std::memcpy(x, in, sizeof(x));
@@ -178,6 +221,25 @@ static void make_cca_pattern(uint32_t* pattern) {
       const hostfft::c16 v = t[i + j];
       pattern[16 * i + j] = (uint32_t)(uint16_t)(v.re >> 7) | ((uint32_t)(uint16_t)(v.im >> 7) << 16);
     }
+}
+
+// createSTSinTime / createLTSinTime at 40 MHz (transmitter/createPreamble.blk:38-117)
+static void make_tx_preamble(uint32_t* out640) {
+  const int16_t sm = (int16_t)(10720.0 * 1.472), lm = 10720;
+  hostfft::c16 f[128] = {}, t[128];
+  const int sp[12] = {4, 8, 12, 16, 20, 24, 104, 108, 112, 116, 120, 124};
+  const int ss[12] = {-1, -1, 1, 1, 1, 1, 1, -1, 1, -1, -1, 1};
+  for (int i = 0; i < 12; i++) f[sp[i]] = {(int16_t)(ss[i] * sm), (int16_t)(ss[i] * sm)};
+  hostfft::ifft128(f, t);
+  auto w = [](hostfft::c16 v) { return (uint32_t)(uint16_t)v.re | ((uint32_t)(uint16_t)v.im << 16); };
+  for (int i = 0; i < 320; i++) out640[i] = w(t[i < 256 ? i & 127 : i - 256]);
+  hostfft::c16 g[128] = {};
+  for (int i = 1; i <= 26; i++) g[i].re = ((kLts11aBits >> i) & 1ull) ? lm : (int16_t)-lm;
+  for (int i = 38; i < 64; i++) g[i + 64].re = ((kLts11aBits >> i) & 1ull) ? lm : (int16_t)-lm;
+  hostfft::ifft128(g, t);
+  uint32_t* l = out640 + 320;
+  for (int i = 0; i < 128; i++) l[64 + i] = l[192 + i] = w(t[i]);
+  for (int i = 0; i < 64; i++) l[i] = l[256 + i];
 }
 
 // amp values where log2(1000 / sqrt(amp)) is an exact k + 0.5 (amp = 10^6 / 2^(2k+1)):
@@ -262,7 +324,8 @@ int zrx_destroy(zrx_ctx* c) {
   free_ws(c);
   (void)hipFree(c->eq_rot);
   (void)hipFree(c->eq_atan);
-  for (void* p : {(void*)c->fe_pattern, (void*)c->fe_syms, (void*)c->fe_sym_off, (void*)c->fe_nsym, (void*)c->fe_chan})
+  for (void* p : {(void*)c->fe_pattern, (void*)c->fe_syms, (void*)c->fe_sym_off, (void*)c->fe_nsym, (void*)c->fe_chan,
+                  (void*)c->tx_preamble})
     (void)hipFree(p);
   (void)hipFree(c->vstream);
   (void)hipFree(c->small);
@@ -456,6 +519,42 @@ int zrx_rx_stream_dev(zrx_ctx* c, const struct complex16* d_samples, const int64
   ZRX_CHECK(hipGetLastError());
   return rx_chain(c, (const complex16*)c->fe_syms, c->fe_sym_off, c->fe_nsym, ncap, max_sym,
                   (const complex16*)c->fe_chan, d_payload, d_info);
+}
+
+int zrx_tx_dev(zrx_ctx* c, const uint8_t* d_in, const int64_t* d_in_off, int npkts, struct complex16* d_out,
+               const int64_t* d_out_off, int32_t* d_nsamp) {
+  if (!c || npkts < 0 || (npkts > 0 && (!d_in || !d_in_off || !d_out || !d_out_off || !d_nsamp))) return ZRX_EINVAL;
+  if (npkts == 0) return ZRX_OK;
+  ZRX_CHECK(hipSetDevice(c->device));
+  if (!c->tx_preamble) {
+    uint32_t pre[640];
+    make_tx_preamble(pre);
+    ZRX_CHECK(hipMalloc(&c->tx_preamble, sizeof(pre)));
+    ZRX_CHECK(hipMemcpy(c->tx_preamble, pre, sizeof(pre), hipMemcpyHostToDevice));
+  }
+  tx::k_tx<<<npkts, 64, 0, c->stream>>>(d_in, d_in_off, npkts, c->tx_preamble, (uint32_t*)d_out, d_out_off, d_nsamp);
+  ZRX_CHECK(hipGetLastError());
+  return ZRX_OK;
+}
+
+int zrx_tx_preamble(int16_t* out1280) {
+  if (!out1280) return ZRX_EINVAL;
+  uint32_t p[640];
+  make_tx_preamble(p);
+  std::memcpy(out1280, p, sizeof(p));
+  return ZRX_OK;
+}
+
+int zrx_tx_samples(const uint8_t* hdr3) {
+  if (!hdr3) return ZRX_EINVAL;
+  const uint32_t hb = (uint32_t)hdr3[0] | ((uint32_t)hdr3[1] << 8) | ((uint32_t)hdr3[2] << 16);
+  static const int nc_of[16] = {0, 0, 0, 0, 0, 0, 0, 0, 288, 192, 96, 48, 288, 192, 96, 48};
+  static const int cr_of[16] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 2, 2, 2, 2};
+  int nc = nc_of[hb & 0xF], cr = cr_of[hb & 0xF];
+  if (!nc) { nc = 48; cr = 0; }                       // parsePLCPHeader default: BPSK 1/2
+  const int nd = cr == 0 ? nc / 2 : cr == 1 ? nc * 2 / 3 : nc * 3 / 4;
+  const int len = std::min((int)((hb >> 5) & 0xFFF), 2048), plen = std::max(len - 4, 0);
+  return 640 + 160 * (1 + (16 + 8 * plen + 32 + 6 + nd - 1) / nd);
 }
 
 int zrx_cca_pattern(int16_t* pattern512) {
@@ -774,6 +873,46 @@ int32_t __ext_wifi_rx_stream_batch(struct complex16* samples, int nsamples, int3
   int ok = 0;
   for (int i = 0; i < nc; i++) ok += det[fe::kDetWords * i] && pkt_info[8 * i + 4] != 0;
   return ok;
+}
+
+int32_t __ext_wifi_tx_batch(unsigned char* in, int inlen, int32_t* pkt_in_off, int n_off,
+                            struct complex16* out, int outlen, int32_t* pkt_out_off, int n_oo) {
+  const int np = n_off - 1;
+  if (np < 0 || inlen < 0 || n_oo < np + 1) return ZRX_EINVAL;
+  if (np == 0) { pkt_out_off[0] = 0; return 0; }
+  std::vector<int64_t> ioff(np), ooff(np);
+  int64_t total = 0;
+  for (int i = 0; i < np; i++) {
+    if (pkt_in_off[i] < 0 || pkt_in_off[i + 1] - pkt_in_off[i] < 3 || pkt_in_off[i + 1] > inlen) return ZRX_EINVAL;
+    const uint8_t* h = in + pkt_in_off[i];
+    const int len = std::min((int)((((uint32_t)h[1] << 8 | h[0]) >> 5 | (uint32_t)h[2] << 11) & 0xFFF), 2048);
+    if (pkt_in_off[i] + 3 + std::max(len - 4, 0) > pkt_in_off[i + 1]) return ZRX_EINVAL;   // payload bytes present
+    ioff[i] = pkt_in_off[i];
+    ooff[i] = total;
+    pkt_out_off[i] = (int32_t)total;
+    total += zrx_tx_samples(h);
+  }
+  pkt_out_off[np] = (int32_t)total;
+  if (total > outlen) return ZRX_EINVAL;
+  std::lock_guard<std::mutex> lk(g_mu);
+  zrx_ctx* c = default_ctx();
+  const size_t s_in = ((size_t)inlen + 255) / 256 * 256 + 256, s_off = ((size_t)np * 8 + 255) / 256 * 256;
+  const size_t s_out = (size_t)total * 4;
+  uint8_t* d = (uint8_t*)staging(c, s_in + 2 * s_off + s_off / 2 + s_out + 1024);
+  if (!d) return ZRX_ENOMEM;
+  uint8_t* d_in = d;
+  int64_t* d_ioff = (int64_t*)(d + s_in);
+  int64_t* d_ooff = (int64_t*)((uint8_t*)d_ioff + s_off);
+  int32_t* d_ns = (int32_t*)((uint8_t*)d_ooff + s_off);
+  uint8_t* d_out = (uint8_t*)d_ns + (s_off / 2 + 255) / 256 * 256;
+  ZRX_CHECK(hipMemcpyAsync(d_in, in, (size_t)inlen, hipMemcpyHostToDevice, c->stream));
+  ZRX_CHECK(hipMemcpyAsync(d_ioff, ioff.data(), (size_t)np * 8, hipMemcpyHostToDevice, c->stream));
+  ZRX_CHECK(hipMemcpyAsync(d_ooff, ooff.data(), (size_t)np * 8, hipMemcpyHostToDevice, c->stream));
+  int rc = zrx_tx_dev(c, d_in, d_ioff, np, (complex16*)d_out, d_ooff, d_ns);
+  if (rc) return rc;
+  ZRX_CHECK(hipMemcpyAsync(out, d_out, s_out, hipMemcpyDeviceToHost, c->stream));
+  ZRX_CHECK(hipStreamSynchronize(c->stream));
+  return (int32_t)total;
 }
 
 }  // extern "C"

@@ -21,6 +21,7 @@
 #include "zrx_viterbi2.hpp"
 #include "zrx_viterbi3.hpp"
 #include "zrx_frontend.hpp"
+#include "zrx_tx.hpp"
 
 namespace zrx {
 

@@ -159,3 +159,19 @@ def wifi_rx_stream_batch(samples, cap_off, downsample=False):
     if rc < 0:
         raise ZiriaRxError(f"__ext_wifi_rx_stream_batch failed ({rc})")
     return pay[:n], {k: info[:n, i].copy() for i, k in enumerate(INFO_FIELDS)}, det[:n], int(rc)
+
+
+def wifi_tx_batch(packets):
+    """transmitter() per packet (transmitter.blk at 40 MHz): packets = list of uint8 arrays,
+    each 3 PLCP header bytes + payload.  Returns (samples int16 [S, 2], offsets int32 [n+1])."""
+    data = np.concatenate([np.asarray(p, np.uint8) for p in packets]) if packets else np.zeros(0, np.uint8)
+    ioff = np.cumsum([0] + [len(p) for p in packets]).astype(np.int32)
+    n = len(packets)
+    total = sum(int(lib().zrx_tx_samples(_p(np.ascontiguousarray(np.asarray(p, np.uint8)[:3])))) for p in packets)
+    out = np.zeros((max(total, 1), 2), np.int16)
+    ooff = np.zeros(n + 1, np.int32)
+    rc = lib().__ext_wifi_tx_batch(_p(np.ascontiguousarray(data)), data.size, _p(ioff), n + 1, _p(out),
+                                   out.shape[0], _p(ooff), n + 1)
+    if rc < 0:
+        raise ZiriaRxError(f"__ext_wifi_tx_batch failed ({rc})")
+    return out[:total], ooff
