@@ -21,6 +21,7 @@ config 2, the batched Viterbi alone (4096 x 1500-byte frames, rate 1/2, soft inp
 2048 are header errors under the reference parser and carry no payload).
 """
 import argparse
+import ctypes as C
 import json
 import os
 import sys
@@ -34,6 +35,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from ziria_amd import node, txgen  # noqa: E402
+from ziria_amd._lib import lib as zlib  # noqa: E402
 from ziria_amd.engine import RxEngine  # noqa: E402
 
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz = 78.6
@@ -64,9 +66,13 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall time budget of the CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 5])
+    ap.add_argument("--tx", action="store_true",
+                    help="TX chain (transmitter() at 40 MHz, SURVEY §8f row 4) on config-3 packets")
     ap.add_argument("--eq", action="store_true",
                     help="config 3 through a channel, with ChannelEqualization + PilotTrack (SURVEY §8f row 1)")
     args = ap.parse_args()
+    if args.tx:
+        return bench_tx(args)
     if args.config == 1:
         return bench_capture(args)
     if args.config == 2:
@@ -347,6 +353,50 @@ def bench_capture(args):
                             "oracle_sample_match": match, "oracle_sample_crc_pass": cpu_ok},
         "cpu_baseline": {"value": round(cpu_bits / cpu_dt / 1e6, 3), "unit": "Mbit/s", "cores": 1,
                          "kind": "port", "sample": f"first {sample} captures, {cpu_dt:.2f} s"},
+    }), flush=True)
+
+
+def bench_tx(args):
+    """transmitter() over config-3 packets (54 Mbps, 1500-byte payloads): header + payload
+    bytes in HBM -> 40 MHz samples in HBM; checked against the oracle on a sample."""
+    import numpy as np
+    from oracle import oracle as O
+    dev = torch.device("cuda", 0)
+    n, L = args.npkts, args.payload
+    rng = np.random.default_rng(0x7E57)
+    hdr = O.plcp_header(3, 2, L + 4)
+    pk = np.concatenate([np.tile(hdr, (n, 1)), rng.integers(0, 256, (n, L)).astype(np.uint8)], 1)
+    per = int(zlib().zrx_tx_samples(hdr.ctypes.data_as(C.c_void_p)))
+    d_in = torch.from_numpy(pk.reshape(-1)).to(dev)
+    d_ioff = torch.arange(n, dtype=torch.int64, device=dev) * (L + 3)
+    d_ooff = torch.arange(n, dtype=torch.int64, device=dev) * per
+    d_out = torch.zeros((n * per, 2), dtype=torch.int16, device=dev)
+    d_ns = torch.zeros(n, dtype=torch.int32, device=dev)
+    eng = RxEngine(0)
+    P = lambda t: C.c_void_p(t.data_ptr())
+
+    def step():
+        eng._stream()
+        rc = zlib().zrx_tx_dev(eng._h, P(d_in), P(d_ioff), n, P(d_out), P(d_ooff), P(d_ns))
+        assert rc == 0, rc
+
+    elapsed = _timed(step, args.steps, args.warmup)
+    out = d_out.cpu().numpy()
+    sample = min(32, n)
+    t0 = time.perf_counter()
+    match = all((out[i * per:(i + 1) * per] == O.tx_packet(pk[i])).all() for i in range(sample))
+    cpu_dt = time.perf_counter() - t0
+    bits = n * L * 8
+    print(json.dumps({
+        "metric": "transmitted payload Mbit/s, 802.11a TX chain at 40 MHz (SURVEY §8f row 4)",
+        "value": round(bits * args.steps / elapsed / 1e6, 1), "unit": "Mbit/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int16",
+        "data": "synthetic payloads", "config": {"workload": f"tx: {n} packets x {L} B @ 54 Mbps, {per} samples each",
+                                                 "gsamples_per_s": round(n * per * args.steps / elapsed / 1e9, 2)},
+        "bit_exact_check": {"oracle_sample_match": bool(match), "sample": sample},
+        "cpu_baseline": {"value": round(sample * L * 8 / cpu_dt / 1e6, 2), "unit": "Mbit/s", "cores": 1,
+                         "kind": "port", "sample": f"first {sample} packets, {cpu_dt:.2f} s (oracle TX + compare)"},
     }), flush=True)
 
 
