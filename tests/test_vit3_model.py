@@ -19,27 +19,30 @@ def test_position_map_is_a_bijection():
                     assert V.lane_of(q) == l ^ V.XOR_OF_BIT[bit]
 
 
+@pytest.mark.parametrize("v4", [False, True])
 @pytest.mark.parametrize("idx", range(0, 48, 5))
-def test_model_matches_reference_frames(golden, idx):
+def test_model_matches_reference_frames(golden, idx, v4):
     g = golden["ref_viterbi"]
     cases, so, oo = g["vit_cases"], g["vit_soft_off"], g["vit_out_off"]
     short = [i for i, c in enumerate(cases) if c[1] <= 333]
     i = short[idx % len(short)]
     cr, fl, _ = cases[i]
-    got = V.decode(g["vit_soft"][so[i]:so[i + 1]], int(fl), int(cr))
+    got = V.decode(g["vit_soft"][so[i]:so[i + 1]], int(fl), int(cr), v4=v4)
     exp = g["vit_out"][oo[i]:oo[i + 1]]
     assert got.size == exp.size and (got == exp).all()
 
 
+@pytest.mark.parametrize("v4", [False, True])
 @pytest.mark.parametrize("cr", [0, 1, 2])
-def test_model_adversarial_wrap(golden, cr):
+def test_model_adversarial_wrap(golden, cr, v4):
     g = golden["ref_viterbi"]
     exp = g[f"vit_adv_out_{cr}"]
-    got = V.decode(g["vit_adv_soft"], 1000, cr)
+    got = V.decode(g["vit_adv_soft"], 1000, cr, v4=v4)
     assert (got[:exp.size] == exp).all()
 
 
-def test_model_truncated_vs_oracle(oracle):
+@pytest.mark.parametrize("v4", [False, True])
+def test_model_truncated_vs_oracle(oracle, v4):
     from tests.golden import synth
     rng = np.random.default_rng(5)
     for i in range(6):
@@ -49,5 +52,5 @@ def test_model_truncated_vs_oracle(oracle):
         if i % 2 == 0:
             s = s[: max(48, (s.size // 2) // 48 * 48)]
         exp = oracle.viterbi_decode(s, fl, cr)
-        got = V.decode(s, fl, cr)
+        got = V.decode(s, fl, cr, v4=v4)
         assert got.size == exp.size and (got == exp).all()

@@ -176,6 +176,46 @@ class Packet:
                         s = rotl6(int(POS[l, d, h]), self.tr)
                         self.ring[slot, s] = (int(self.M[l, d]) >> (16 * h)) & 0xFF
 
+    def step4(self, kind, a, b):
+        """v4 column: one v_add_u32 per candidate instead of v_pk_add_u16, the cross
+        candidate added straight from the partner lane (v_add_u32_dpp) with the complement
+        branch metric C - BX of this position (the partner state j ^ 32 has the same expected
+        bits and the other marker), pads cleared after each snapshot.  A 32-bit add carries
+        out of half 0 into bit 0 of half 1's pad when H0 wraps; that bit is 0 at every
+        non-snapshot column (cleared 1..7 columns earlier) and is never read, and the
+        snapshot column itself uses exact packed adds."""
+        ph = self.tr % 6
+        c = self.tr + 1                                   # column being computed
+        M = self.M
+        if c % 8 == 7:                                    # first column after a snapshot
+            T = (M & 0xFF00FF00).astype(np.uint32)
+        else:
+            T = (((M >> 1) & 0x00FF00FF) | (M & 0xFF00FF00)).astype(np.uint32)
+        if c % 8 != 7 and c % 8 != 6:
+            assert ((T >> 16) & 1).max() == 0, "half-1 guard bit set at a 32-bit add"
+        BX = perm(0x80808080, p_word(kind, a, b), SEL[ph])
+        C = 0x1C801C80 if kind == FULL else 0x0E800E80
+        BY = ((C - BX.astype(np.int64)) & 0xFFFFFFFF).astype(np.uint32)
+        exact = c % 8 == 6
+        add = pk_add if exact else (lambda x, y: ((x.astype(np.uint64) + y) & 0xFFFFFFFF).astype(np.uint32))
+        if ph <= 3:
+            Tp = T[np.arange(16) ^ XOR_OF_BIT[5 - ph]]
+            Z = add(Tp, BY)
+        elif ph == 4:
+            Z = add(T[:, ::-1], BY)
+        else:
+            Z = pk_add(swap_halves(T), BY)
+        X = add(T, BX)
+        self.M = pk_min(X, Z)
+        self.tr += 1
+        if self.tr % 8 == 6:
+            slot = ((self.tr - 6) // 8) % RING
+            for l in range(16):
+                for d in range(2):
+                    for h in range(2):
+                        s = rotl6(int(POS[l, d, h]), self.tr)
+                        self.ring[slot, s] = (int(self.M[l, d]) >> (16 * h)) & 0xFF
+
     def normalize(self):
         H = np.concatenate([(self.M & 0xFFFF).ravel(), (self.M >> 16).ravel()]) >> 8
         mn = int(H.min())
@@ -210,9 +250,11 @@ class Packet:
         return [blocks[c] for c in range(c_first, c_hi + 1, 8)]
 
 
-def decode(soft, frame_len, code_rate):
-    """Model of one packet through k_viterbi3 (whole soft buffer, 24-column bodies)."""
+def decode(soft, frame_len, code_rate, v4=False):
+    """Model of one packet through k_viterbi3 (whole soft buffer, 24-column bodies);
+    v4 = the carry-tolerant 32-bit-add column (Packet.step4)."""
     P = Packet(frame_len, code_rate)
+    stepf = P.step4 if v4 else P.step
     kinds = KINDS[code_rate]
     G = {0: 2, 1: 3, 2: 4}[code_rate]
     soft = np.asarray(soft, np.int64)
@@ -221,7 +263,7 @@ def decode(soft, frame_len, code_rate):
         s = soft[g * G:(g + 1) * G]
         args = [(s[0], s[1])] + [(v, 0) for v in s[2:]]
         for k, kind in enumerate(kinds):
-            P.step(kind, *args[k])
+            stepf(kind, *args[k])
         if P.tr % 8 == 0:
             P.normalize()
         if P.tr >= P.end:

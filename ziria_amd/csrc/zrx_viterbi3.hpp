@@ -119,6 +119,60 @@ __device__ __forceinline__ void column(uint32_t& M0, uint32_t& M1, uint32_t P, c
   }
 }
 
+// The same column with 32-bit adds (tests/vit3_model.py Packet.step4).  The cross candidate
+// is the partner's shifted metric plus this position's complement metric C - BX: the
+// partner state j ^ 32 has the same expected bits (A, B depend on j bits 0..4) and the
+// other marker, so C = (k << 8) | 0x80 per half is one lane-uniform literal and the partner
+// lane's T is read straight by v_add_u32_dpp (no v_mov_dpp, no v_pk_add_u16).  A 32-bit
+// add carries out of half 0 into bit 0 of half 1's pad when H0 + BM wraps; MODE keeps that
+// bit 0 at every such add: MODE 1 (the column after a snapshot) clears the pads instead of
+// shifting them, so the oldest history bit reaching bit 0 is the one already stored, and
+// MODE 2 (the snapshot column, where bit 0 is a live decision) adds exactly with
+// v_pk_add_u16.  A set bit 0 is below the marker (never decides a min) and is shifted out
+// before anything reads it.  SDWA: shift each pad in place with v_lshrrev_b16 SDWA.
+template <int PH, int KIND, int MODE, bool SDWA>
+__device__ __forceinline__ void column4(uint32_t& M0, uint32_t& M1, uint32_t P, const Consts& K) {
+  uint32_t T0, T1;
+  if constexpr (MODE == 1) {
+    T0 = M0 & 0xFF00FF00u;
+    T1 = M1 & 0xFF00FF00u;
+  } else if constexpr (SDWA) {
+    T0 = M0; T1 = M1;
+    asm("v_lshrrev_b16_sdwa %0, 1, %0 dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src1_sel:WORD_0\n\t"
+        "v_lshrrev_b16_sdwa %0, 1, %0 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src1_sel:WORD_1"
+        : "+v"(T0));
+    asm("v_lshrrev_b16_sdwa %0, 1, %0 dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src1_sel:WORD_0\n\t"
+        "v_lshrrev_b16_sdwa %0, 1, %0 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src1_sel:WORD_1"
+        : "+v"(T1));
+  } else {
+    T0 = ((M0 >> 1) & 0x00FF00FFu) | (M0 & 0xFF00FF00u);
+    T1 = ((M1 >> 1) & 0x00FF00FFu) | (M1 & 0xFF00FF00u);
+  }
+  constexpr uint32_t C = KIND == 0 ? 0x1C801C80u : 0x0E800E80u;
+  const uint32_t BX0 = __builtin_amdgcn_perm(0x80808080u, P, K.sel[PH][0]);
+  const uint32_t BX1 = __builtin_amdgcn_perm(0x80808080u, P, K.sel[PH][1]);
+  const uint32_t BY0 = C - BX0, BY1 = C - BX1;
+  auto add = [](uint32_t a, uint32_t b) -> uint32_t {
+    if constexpr (MODE == 2) return w32(h2(a) + h2(b));
+    else return a + b;
+  };
+  const uint32_t X0 = add(T0, BX0), X1 = add(T1, BX1);
+  uint32_t Z0, Z1;
+  if constexpr (PH <= 3) {
+    constexpr int ctrl = PH == 0 ? 0x128 : PH == 1 ? 0x140 : PH == 2 ? 0x4E : 0xB1;  // xor 8, 15, 2, 1
+    Z0 = add((uint32_t)__builtin_amdgcn_mov_dpp((int)T0, ctrl, 0xF, 0xF, true), BY0);
+    Z1 = add((uint32_t)__builtin_amdgcn_mov_dpp((int)T1, ctrl, 0xF, 0xF, true), BY1);
+  } else if constexpr (PH == 4) {
+    Z0 = add(T1, BY0);
+    Z1 = add(T0, BY1);
+  } else {
+    Z0 = w32(h2(T0).yx + h2(BY0));
+    Z1 = w32(h2(T1).yx + h2(BY1));
+  }
+  M0 = w32(__builtin_elementwise_min(h2(X0), h2(Z0)));
+  M1 = w32(__builtin_elementwise_min(h2(X1), h2(Z1)));
+}
+
 // normalize (viterbicore.hpp:149-168): H -= min over the row's 64 H bytes (H even).
 __device__ __forceinline__ void normalize(uint32_t& M0, uint32_t& M1) {
   const u16x2 t = __builtin_elementwise_min(h2(M0), h2(M1));
@@ -233,7 +287,7 @@ __device__ __forceinline__ uint32_t p_word(uint32_t r, uint32_t a, uint32_t b) {
 // DBG (timing experiments only, never selected by default): 1 skip the traceback walk,
 // 2 skip snapshot stores, 4 skip normalization, 8 no P broadcast, 16 never run checked bodies,
 // 32 broadcast P with DPP row_newbcast, 64 ds_swizzle issued 4 columns ahead behind a
-// scheduling barrier.
+// scheduling barrier, 128 the v3 column (packed adds + v_mov_dpp), 256 SDWA pad shifts.
 template <int CR, int DBG = 0>
 struct Packet {
   using RT = Rate<CR>;
@@ -263,8 +317,11 @@ struct Packet {
       if constexpr ((DBG & 64) != 0) __builtin_amdgcn_sched_barrier(0);
     }
     constexpr int r = J % RT::steps;
-    column<J % 6, r>(M0, M1, P, K);
     constexpr int c = J + 1;                           // column index within the body after the step
+    if constexpr ((DBG & 128) != 0)
+      column<J % 6, r>(M0, M1, P, K);
+    else
+      column4<J % 6, r, c % 8 == 6 ? 2 : c % 8 == 7 ? 1 : 0, (DBG & 256) != 0>(M0, M1, P, K);
     if constexpr (c % 8 == 6 && !(DBG & 2)) {          // snapshot column (C = 6 mod 8)
       uint8_t* s = ring + (c >> 3) * kSlotBytes;
       s[K.sa[c >> 3][0]] = (uint8_t)M0;
