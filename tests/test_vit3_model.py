@@ -19,7 +19,7 @@ def test_position_map_is_a_bijection():
                     assert V.lane_of(q) == l ^ V.XOR_OF_BIT[bit]
 
 
-@pytest.mark.parametrize("v4", [False, True])
+@pytest.mark.parametrize("v4", [False, True, 5])
 @pytest.mark.parametrize("idx", range(0, 48, 5))
 def test_model_matches_reference_frames(golden, idx, v4):
     g = golden["ref_viterbi"]
@@ -32,7 +32,7 @@ def test_model_matches_reference_frames(golden, idx, v4):
     assert got.size == exp.size and (got == exp).all()
 
 
-@pytest.mark.parametrize("v4", [False, True])
+@pytest.mark.parametrize("v4", [False, True, 5])
 @pytest.mark.parametrize("cr", [0, 1, 2])
 def test_model_adversarial_wrap(golden, cr, v4):
     g = golden["ref_viterbi"]
@@ -41,7 +41,7 @@ def test_model_adversarial_wrap(golden, cr, v4):
     assert (got[:exp.size] == exp).all()
 
 
-@pytest.mark.parametrize("v4", [False, True])
+@pytest.mark.parametrize("v4", [False, True, 5])
 def test_model_truncated_vs_oracle(oracle, v4):
     from tests.golden import synth
     rng = np.random.default_rng(5)

@@ -150,6 +150,7 @@ class Packet:
         self.end = 8 * frame_len + 6
         self.out = []
         self.done = False
+        self.v5 = False
 
     def step(self, kind, a, b):
         ph = self.tr % 6
@@ -216,6 +217,47 @@ class Packet:
                         s = rotl6(int(POS[l, d, h]), self.tr)
                         self.ring[slot, s] = (int(self.M[l, d]) >> (16 * h)) & 0xFF
 
+    def step5(self, kind, a, b):
+        """v5 column: no pad shift.  The column with cycle phase k = (c + 1) % 8 (c = the
+        column being computed; k = 7 is the snapshot column) writes its marker at bit k + 1
+        of each half, so a half is [H >> 1 (bits 15..9)][decisions of the cycle, bits 8..1,
+        oldest lowest][bit 0: carry guard].  Bits above the marker are still 0 in both
+        candidates (cleared at k = 0), so the marker decides ties exactly as the brick's
+        metric LSB (viterbicore.hpp:105-147); a snapshot byte is bits 8..1.  The 32-bit adds
+        carry out of half 0 into bit 16 only, which one AND per column clears (k = 0: the AND
+        also clears the cycle's history).  At k = 7 the marker is bit 8, the H byte's LSB
+        (H is even): BX = [BM][bm<<7] + (its low byte) = [BM + bm][0]."""
+        ph = self.tr % 6
+        c = self.tr + 1
+        k = (c + 1) % 8
+        M = self.M
+        T = (M & (0xFE00FE00 if k == 0 else 0xFFFEFFFF)).astype(np.uint32)
+        mk = 2 << k
+        src0 = 0x80808080 if k == 7 else mk * 0x01010101
+        BX = perm(src0, p_word(kind, a, b), SEL[ph])
+        if k == 7:
+            BX = (BX + (BX & 0x00FF00FF)).astype(np.uint32)
+        K = 28 if kind == FULL else 14
+        C = ((K + 1) << 8) * 0x00010001 if k == 7 else ((K << 8) | mk) * 0x00010001
+        BY = ((C - BX.astype(np.int64)) & 0xFFFFFFFF).astype(np.uint32)
+        add = lambda x, y: ((x.astype(np.uint64) + y) & 0xFFFFFFFF).astype(np.uint32)
+        if ph <= 3:
+            Z = add(T[np.arange(16) ^ XOR_OF_BIT[5 - ph]], BY)
+        elif ph == 4:
+            Z = add(T[:, ::-1], BY)
+        else:
+            Z = pk_add(swap_halves(T), BY)
+        X = add(T, BX)
+        self.M = pk_min(X, Z)
+        self.tr += 1
+        if self.tr % 8 == 6:
+            slot = ((self.tr - 6) // 8) % RING
+            for l in range(16):
+                for d in range(2):
+                    for h in range(2):
+                        s = rotl6(int(POS[l, d, h]), self.tr)
+                        self.ring[slot, s] = (int(self.M[l, d]) >> (16 * h + 1)) & 0xFF
+
     def normalize(self):
         H = np.concatenate([(self.M & 0xFFFF).ravel(), (self.M >> 16).ravel()]) >> 8
         mn = int(H.min())
@@ -228,7 +270,13 @@ class Packet:
                 for h in range(2):
                     half = (int(Mt[l, d]) >> (16 * h)) & 0xFFFF
                     s = rotl6(int(POS[l, d, h]), T)
-                    m = (half >> 8) | ((half >> 7) & 1)
+                    if self.v5:                           # marker of column T at bit (T+1)%8 + 1
+                        m = ((half >> 8) & 0xFE) | ((half >> ((T + 1) % 8 + 1)) & 1)
+                        n = (T - 6) % 8                   # decisions since the snapshot, bits n..1
+                        pad = (((half >> 1) & ((1 << n) - 1)) << (8 - n)) & 0xFF
+                        half = (half & 0xFF00) | pad       # the v3 pad form
+                    else:
+                        m = (half >> 8) | ((half >> 7) & 1)
                     key = ((m << 8) | (4 * s)) & 0xFFFF
                     key = key - 65536 if key >= 32768 else key
                     if best is None or key < best[0]:
@@ -252,9 +300,11 @@ class Packet:
 
 def decode(soft, frame_len, code_rate, v4=False):
     """Model of one packet through k_viterbi3 (whole soft buffer, 24-column bodies);
-    v4 = the carry-tolerant 32-bit-add column (Packet.step4)."""
+    v4 = the carry-tolerant 32-bit-add column (Packet.step4), v4 = 5 the shift-free
+    ascending-marker column (Packet.step5)."""
     P = Packet(frame_len, code_rate)
-    stepf = P.step4 if v4 else P.step
+    P.v5 = v4 == 5
+    stepf = P.step5 if v4 == 5 else P.step4 if v4 else P.step
     kinds = KINDS[code_rate]
     G = {0: 2, 1: 3, 2: 4}[code_rate]
     soft = np.asarray(soft, np.int64)

@@ -286,7 +286,7 @@ static void launch_viterbi(zrx_ctx* c, const uint8_t* soft, const int64_t* soft_
     const dim3 g(blocks(npkts, v3::kRows)), b(256);
     switch (c->v3dbg) {   // timing experiments only (ZRX_V3DBG); 0 is the product kernel
 #define ZRX_V3(D) case D: k_viterbi3<D><<<g, b, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits, order); break;
-      ZRX_V3(1) ZRX_V3(2) ZRX_V3(4) ZRX_V3(8) ZRX_V3(16) ZRX_V3(32) ZRX_V3(64) ZRX_V3(128) ZRX_V3(256)
+      ZRX_V3(1) ZRX_V3(2) ZRX_V3(4) ZRX_V3(8) ZRX_V3(16) ZRX_V3(32) ZRX_V3(64) ZRX_V3(128) ZRX_V3(256) ZRX_V3(512)
 #undef ZRX_V3
       default: k_viterbi3<0><<<g, b, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits, order);
     }

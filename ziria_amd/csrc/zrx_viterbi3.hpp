@@ -173,6 +173,50 @@ __device__ __forceinline__ void column4(uint32_t& M0, uint32_t& M1, uint32_t P, 
   M1 = w32(__builtin_elementwise_min(h2(X1), h2(Z1)));
 }
 
+// Shift-free column (tests/vit3_model.py Packet.step5).  The column with cycle phase KPH =
+// (c + 1) mod 8 (c = the column computed; KPH 7 is the snapshot column) writes its marker at
+// bit KPH + 1 of each half: a half is [H >> 1 in bits 15..9][the cycle's decisions in bits
+// 8..1, oldest lowest][bit 0: carry guard].  Bits above the marker are still 0 in both
+// candidates (cleared at KPH 0), so the marker breaks ties exactly like the brick's metric
+// LSB (viterbicore.hpp:105-147), and the pads need no shift: one AND per dword clears the
+// guard bit 16 that a 32-bit add carries into when H0 wraps (at KPH 0 it also clears the
+// cycle's history).  At KPH 7 the marker is bit 8, the LSB of the (even) H byte: BX =
+// [BM][bm << 7] plus its own low byte = [BM + bm][0].
+template <int PH, int KIND, int KPH>
+__device__ __forceinline__ void column5(uint32_t& M0, uint32_t& M1, uint32_t P, const Consts& K) {
+  constexpr uint32_t mask = KPH == 0 ? 0xFE00FE00u : 0xFFFEFFFFu;
+  const uint32_t T0 = M0 & mask, T1 = M1 & mask;
+  constexpr uint32_t mk = 2u << KPH;
+  constexpr uint32_t Kc = KIND == 0 ? 28u : 14u;
+  constexpr uint32_t C = KPH == 7 ? ((Kc + 1u) << 8) * 0x00010001u : ((Kc << 8) | mk) * 0x00010001u;
+  uint32_t BX0, BX1;
+  if constexpr (KPH == 7) {
+    BX0 = __builtin_amdgcn_perm(0x80808080u, P, K.sel[PH][0]);
+    BX1 = __builtin_amdgcn_perm(0x80808080u, P, K.sel[PH][1]);
+    BX0 += BX0 & 0x00FF00FFu;
+    BX1 += BX1 & 0x00FF00FFu;
+  } else {
+    BX0 = __builtin_amdgcn_perm((mk & 0xFFu) * 0x01010101u, P, K.sel[PH][0]);
+    BX1 = __builtin_amdgcn_perm((mk & 0xFFu) * 0x01010101u, P, K.sel[PH][1]);
+  }
+  const uint32_t BY0 = C - BX0, BY1 = C - BX1;
+  const uint32_t X0 = T0 + BX0, X1 = T1 + BX1;
+  uint32_t Z0, Z1;
+  if constexpr (PH <= 3) {
+    constexpr int ctrl = PH == 0 ? 0x128 : PH == 1 ? 0x140 : PH == 2 ? 0x4E : 0xB1;  // xor 8, 15, 2, 1
+    Z0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)T0, ctrl, 0xF, 0xF, true) + BY0;
+    Z1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)T1, ctrl, 0xF, 0xF, true) + BY1;
+  } else if constexpr (PH == 4) {
+    Z0 = T1 + BY0;
+    Z1 = T0 + BY1;
+  } else {
+    Z0 = w32(h2(T0).yx + h2(BY0));
+    Z1 = w32(h2(T1).yx + h2(BY1));
+  }
+  M0 = w32(__builtin_elementwise_min(h2(X0), h2(Z0)));
+  M1 = w32(__builtin_elementwise_min(h2(X1), h2(Z1)));
+}
+
 // normalize (viterbicore.hpp:149-168): H -= min over the row's 64 H bytes (H even).
 __device__ __forceinline__ void normalize(uint32_t& M0, uint32_t& M1) {
   const u16x2 t = __builtin_elementwise_min(h2(M0), h2(M1));
@@ -233,6 +277,7 @@ __device__ __forceinline__ void events(Row& R, uint32_t tr, uint32_t M0, uint32_
 // then one lane per row walks the snapshot ring and writes the window's bytes.  The walk is
 // a chain of dependent LDS reads (state -> byte -> state 8 columns back), so the loop body
 // keeps only the read, the bit reversal and the address add on that chain.
+template <bool V5>
 __device__ __forceinline__ void traceback(bool due, uint32_t M0, uint32_t M1, uint32_t T, uint32_t cnt,
                                           uint32_t look, uint32_t l, uint32_t rib, const uint8_t* ring,
                                           uint8_t* __restrict__ out, uint32_t ooff, uint32_t& nbytes) {
@@ -242,9 +287,17 @@ __device__ __forceinline__ void traceback(bool due, uint32_t M0, uint32_t M1, ui
   for (int q = 0; q < 4; q++) {
     const uint32_t half = ((q >> 1) ? M1 : M0) >> (16 * (q & 1)) & 0xFFFFu;
     const uint32_t st = rotl6(pos_of(l, q >> 1, q & 1), ph);
-    const uint32_t m = (half >> 8) | ((half >> 7) & 1u);
+    uint32_t m, pad;
+    if constexpr (V5) {   // marker of column T at bit (T+1)%8 + 1; the n = (T-6)%8 newest decisions in bits n..1
+      const uint32_t n = (T - 6u) & 7u;
+      m = ((half >> 8) & 0xFEu) | ((half >> (((T + 1u) & 7u) + 1u)) & 1u);
+      pad = (((half >> 1) & ((1u << n) - 1u)) << (8u - n)) & 0xFFu;   // as the shifted pad: newest at bit 7
+    } else {
+      m = (half >> 8) | ((half >> 7) & 1u);
+      pad = half & 0xFFu;
+    }
     const uint32_t ukey = (((m << 8) | (st << 2)) & 0xFFFFu) ^ 0x8000u;   // signed int16 order
-    best = min(best, (ukey << 16) | (half & 0xFFu));
+    best = min(best, (ukey << 16) | pad);
   }
   best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0xB1, 0xF, 0xF, false));
   best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x4E, 0xF, 0xF, false));
@@ -287,10 +340,13 @@ __device__ __forceinline__ uint32_t p_word(uint32_t r, uint32_t a, uint32_t b) {
 // DBG (timing experiments only, never selected by default): 1 skip the traceback walk,
 // 2 skip snapshot stores, 4 skip normalization, 8 no P broadcast, 16 never run checked bodies,
 // 32 broadcast P with DPP row_newbcast, 64 ds_swizzle issued 4 columns ahead behind a
-// scheduling barrier, 128 the v3 column (packed adds + v_mov_dpp), 256 SDWA pad shifts.
+// scheduling barrier, 128 the v3 column (packed adds + v_mov_dpp), 256 SDWA pad shifts,
+// 512 the shifted-pad 32-bit-add column (column4, the previous default).  128/256/512 are
+// exact (other layouts), the rest are timing-only.
 template <int CR, int DBG = 0>
 struct Packet {
   using RT = Rate<CR>;
+  static constexpr bool V5 = (DBG & (128 | 256 | 512)) == 0;   // shift-free column (default)
   const Consts& K;
   Row& R;
   uint32_t l, rib;
@@ -318,16 +374,19 @@ struct Packet {
     }
     constexpr int r = J % RT::steps;
     constexpr int c = J + 1;                           // column index within the body after the step
-    if constexpr ((DBG & 128) != 0)
+    if constexpr (V5)
+      column5<J % 6, r, (J + 2) % 8>(M0, M1, P, K);
+    else if constexpr ((DBG & 128) != 0)
       column<J % 6, r>(M0, M1, P, K);
     else
       column4<J % 6, r, c % 8 == 6 ? 2 : c % 8 == 7 ? 1 : 0, (DBG & 256) != 0>(M0, M1, P, K);
     if constexpr (c % 8 == 6 && !(DBG & 2)) {          // snapshot column (C = 6 mod 8)
       uint8_t* s = ring + (c >> 3) * kSlotBytes;
-      s[K.sa[c >> 3][0]] = (uint8_t)M0;
-      s[K.sa[c >> 3][1]] = (uint8_t)(M0 >> 16);
-      s[K.sa[c >> 3][2]] = (uint8_t)M1;
-      s[K.sa[c >> 3][3]] = (uint8_t)(M1 >> 16);
+      constexpr int sh = V5 ? 1 : 0;                   // v5: the decisions are bits 8..1
+      s[K.sa[c >> 3][0]] = (uint8_t)(M0 >> sh);
+      s[K.sa[c >> 3][1]] = (uint8_t)(M0 >> (16 + sh));
+      s[K.sa[c >> 3][2]] = (uint8_t)(M1 >> sh);
+      s[K.sa[c >> 3][3]] = (uint8_t)(M1 >> (16 + sh));
     }
     if constexpr (c % RT::steps == 0) {                // group end
       if constexpr (c % 8 == 0 && (CR != 2 || c == 24) && !(DBG & 4)) normalize(M0, M1);
@@ -396,11 +455,11 @@ __device__ void run_rows(const uint8_t* __restrict__ sp, uint32_t n, Row& R, con
       pk.template body<true>(M0, M1, Pa, Pb, tr0, s_next, std::make_integer_sequence<int, 24>{});
     slot = slot + 3 == kRing ? 0 : slot + 3;
     if ((DBG & 1) == 0 && __builtin_amdgcn_ballot_w64(R.ppend) != 0) {
-      traceback(R.ppend, R.pM0, R.pM1, R.pT, 256u, R.plook, l, rib, ring_block, out, ooff, R.nbytes);
+      traceback<Packet<CR, DBG>::V5>(R.ppend, R.pM0, R.pM1, R.pT, 256u, R.plook, l, rib, ring_block, out, ooff, R.nbytes);
       R.ppend = false;
     }
     if ((DBG & 1) == 0 && __builtin_amdgcn_ballot_w64(R.fpend) != 0) {
-      traceback(R.fpend, R.fM0, R.fM1, R.fT, R.fcnt, R.flook, l, rib, ring_block, out, ooff, R.nbytes);
+      traceback<Packet<CR, DBG>::V5>(R.fpend, R.fM0, R.fM1, R.fT, R.fcnt, R.flook, l, rib, ring_block, out, ooff, R.nbytes);
       R.fpend = false;
     }
     if constexpr ((DBG & 1) != 0) R.ppend = R.fpend = false;
