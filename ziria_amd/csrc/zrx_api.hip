@@ -51,6 +51,9 @@ struct zrx_ctx {
   int32_t* dec_bits = nullptr;
   int32_t* order = nullptr;       // Viterbi packet order (k_vit_order)
   bool use_order = true;          // ZRX_ORDER=0 turns the ordering off (A/B experiments)
+  // rx chain: k_vit_order runs on a side stream beside k_data_fft (fork/join by events)
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
   // ChannelEqualization / PilotTrack trig tables (built on first use)
   uint32_t* eq_rot = nullptr;     // 65536 x (cos, -sin) complex16
   int16_t* eq_atan = nullptr;     // 256 x 256 atan2x_lut
@@ -271,13 +274,19 @@ static int ensure_eq_tables(zrx_ctx* c) {
   return ZRX_OK;
 }
 
+static bool order_fits(const zrx_ctx* c, int npkts) {
+  return c->vit_impl == 3 && c->use_order && c->order && npkts <= c->cap_pkts && npkts <= kOrderMax;
+}
+
+// order_ready: the caller already ran k_vit_order into c->order (rx chain, side stream)
 static void launch_viterbi(zrx_ctx* c, const uint8_t* soft, const int64_t* soft_off, const int32_t* params,
-                           int npkts, uint8_t* out, const int64_t* out_off, int32_t* out_bits) {
+                           int npkts, uint8_t* out, const int64_t* out_off, int32_t* out_bits,
+                           bool order_ready = false) {
   // rows of a k_viterbi3 wave should share a rate and length: order the batch first when the
   // workspace has room for it (zrx_reserve); otherwise identity order (still exact)
   const int32_t* order = nullptr;
-  if (c->vit_impl == 3 && c->use_order && c->order && npkts <= c->cap_pkts && npkts <= kOrderMax) {
-    k_vit_order<<<1, 1024, 0, c->stream>>>(params, npkts, c->order);
+  if (order_fits(c, npkts)) {
+    if (!order_ready) k_vit_order<<<1, 1024, 0, c->stream>>>(params, npkts, c->order);
     order = c->order;
   }
   if (c->vit_impl == 1)
@@ -329,6 +338,12 @@ int zrx_destroy(zrx_ctx* c) {
     (void)hipFree(p);
   (void)hipFree(c->vstream);
   (void)hipFree(c->small);
+  if (c->side) {
+    (void)hipStreamSynchronize(c->side);
+    (void)hipStreamDestroy(c->side);
+    (void)hipEventDestroy(c->fork);
+    (void)hipEventDestroy(c->join);
+  }
   for (auto& set : c->evsets)
     for (auto& e : set) (void)hipEventDestroy(e);
   delete c;
@@ -441,6 +456,20 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
   if (ev) ZRX_CHECK(hipEventRecord(ev[1], s));
   k_signal_vit<<<blocks(npkts, 4), 256, 0, s>>>(c->sig_soft, d_nsym, npkts, c->vparams, d_info);
   if (ev) ZRX_CHECK(hipEventRecord(ev[2], s));
+  // the Viterbi packet order needs only the headers: one block on the side stream, hidden
+  // behind k_data_fft (a 1-block kernel costs ~20 us in line)
+  const bool side_order = order_fits(c, npkts);
+  if (side_order) {
+    if (!c->side) {
+      ZRX_CHECK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+      ZRX_CHECK(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
+      ZRX_CHECK(hipEventCreateWithFlags(&c->join, hipEventDisableTiming));
+    }
+    ZRX_CHECK(hipEventRecord(c->fork, s));
+    ZRX_CHECK(hipStreamWaitEvent(c->side, c->fork, 0));
+    k_vit_order<<<1, 1024, 0, c->side>>>(c->vparams, npkts, c->order);
+    ZRX_CHECK(hipEventRecord(c->join, c->side));
+  }
   if (chan)
     k_data_fft<true><<<blocks(npkts, 4), 256, 0, s>>>((const uint4*)d_sym, d_sym_off, c->vparams, npkts,
                                                       (uint4*)c->soft, c->soft_off, chan, T);
@@ -448,7 +477,8 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
     k_data_fft<false><<<blocks(npkts, 4), 256, 0, s>>>((const uint4*)d_sym, d_sym_off, c->vparams, npkts,
                                                        (uint4*)c->soft, c->soft_off, chan, T);
   if (ev) ZRX_CHECK(hipEventRecord(ev[3], s));
-  launch_viterbi(c, c->soft, c->soft_off, c->vparams, npkts, c->dec, c->dec_off, c->dec_bits);
+  if (side_order) ZRX_CHECK(hipStreamWaitEvent(s, c->join, 0));
+  launch_viterbi(c, c->soft, c->soft_off, c->vparams, npkts, c->dec, c->dec_off, c->dec_bits, side_order);
   if (ev) ZRX_CHECK(hipEventRecord(ev[4], s));
   k_descramble_crc<<<blocks(npkts, kCrcWaves), 64 * kCrcWaves, 0, s>>>(c->dec, c->dec_bits, d_info, d_payload, npkts);
   if (ev) ZRX_CHECK(hipEventRecord(ev[5], s));

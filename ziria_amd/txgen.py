@@ -204,10 +204,20 @@ def make_batch(n, mod=3, coding=2, payload_len=1500, sigma=4.0, seed=0x5EED, dev
 MCS8 = [(0, 0), (0, 2), (1, 0), (1, 2), (2, 0), (2, 2), (3, 1), (3, 2)]
 
 
-def make_mixed(n, min_len=64, max_len=4095, sigma=4.0, seed=0x3C5, device="cpu"):
+def make_mixed(n, min_len=64, max_len=4095, sigma=4.0, seed=0x3C5, device="cpu", unique=None):
     """BASELINE config 5: MCS uniform over the 8 rates, PSDU length (the PLCP LENGTH field,
     payload + 4 CRC bytes) uniform in [min_len, max_len].  Lengths > 2048 are header errors
-    under the reference parser (parsePLCPHeader.blk:171-174) and decode to no payload."""
+    under the reference parser (parsePLCPHeader.blk:171-174) and decode to no payload.
+    unique < n: generate `unique` packets (one TX per packet is slow) and tile them."""
+    if unique is not None and unique < n:
+        m = make_mixed(unique, min_len, max_len, sigma, seed, device)
+        reps = (n + unique - 1) // unique
+        S = m["sym"].shape[0]
+        idx = torch.arange(n, device=device) % unique
+        offs = m["sym_off"][idx] + (torch.arange(n, device=device) // unique) * S
+        return dict(sym=m["sym"].repeat(reps, 1, 1), sym_off=offs, nsym=m["nsym"][idx],
+                    payload=[m["payload"][i % unique] for i in range(n)],
+                    meta=m["meta"][np.arange(n) % unique], max_nsym=m["max_nsym"])
     rng = np.random.default_rng(seed)
     gen = torch.Generator(device=device)
     gen.manual_seed(seed)
