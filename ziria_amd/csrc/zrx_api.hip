@@ -31,6 +31,7 @@ using namespace zrx;
 
 struct zrx_ctx {
   int device = 0;
+  int crc_blocks = 1024;          // ZRX_CRCBLOCKS: k_descramble_crc grid cap (0 = one packet per wave)
   int v3dbg = 0;                  // ZRX_V3DBG: k_viterbi3 timing-experiment variants (wrong output)
   int vit_impl = 3;              // 3: k_viterbi3 (default); 2: k_viterbi2; 1: k_viterbi (A/B references)
   hipStream_t stream = nullptr;
@@ -323,6 +324,7 @@ int zrx_create(zrx_ctx** out, int device, void* stream) {
   }
   if (const char* v = std::getenv("ZRX_V3DBG")) c->v3dbg = std::atoi(v);
   if (const char* v = std::getenv("ZRX_ORDER")) c->use_order = std::atoi(v) != 0;
+  if (const char* v = std::getenv("ZRX_CRCBLOCKS")) c->crc_blocks = std::atoi(v);
   *out = c;
   return ZRX_OK;
 }
@@ -480,7 +482,8 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
   if (side_order) ZRX_CHECK(hipStreamWaitEvent(s, c->join, 0));
   launch_viterbi(c, c->soft, c->soft_off, c->vparams, npkts, c->dec, c->dec_off, c->dec_bits, side_order);
   if (ev) ZRX_CHECK(hipEventRecord(ev[4], s));
-  k_descramble_crc<<<blocks(npkts, kCrcWaves), 64 * kCrcWaves, 0, s>>>(c->dec, c->dec_bits, d_info, d_payload, npkts);
+  k_descramble_crc<<<c->crc_blocks > 0 ? std::min(blocks(npkts, kCrcWaves), c->crc_blocks) : blocks(npkts, kCrcWaves),
+                     64 * kCrcWaves, 0, s>>>(c->dec, c->dec_bits, d_info, d_payload, npkts);
   if (ev) ZRX_CHECK(hipEventRecord(ev[5], s));
   ZRX_CHECK(hipGetLastError());
   return ZRX_OK;

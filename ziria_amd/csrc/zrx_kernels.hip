@@ -377,88 +377,90 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
   for (int i = threadIdx.x; i < 127; i += blockDim.x) scrw[i] = kScrW[i];
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int p = blockIdx.x * kCrcWaves + wv;
-  if (p >= npkts) return;
-  int32_t* in = info + 8 * (int64_t)p;
-  const int len = in[2], status = in[5];
-  const int bits = dec_bits[p];
-  if (lane == 0) in[7] = bits;
-  if (status != 0 || bits < (len + 2) * 8 || len < 4) {
-    if (lane == 0) in[4] = 0;
-    return;
-  }
-  const uint8_t* d = dec + (int64_t)p * kDecStride;
-  const uint32_t* d32 = (const uint32_t*)d;
-  uint32_t* py32 = (uint32_t*)(payload + (int64_t)p * kPayloadStride);
-  const uint32_t S = (uint32_t)d[1] >> 1;           // SERVICE bits 9..15 = scrambler state
-  const uint32_t ksm = S == 0 ? 0u : 0xFFFFFFFFu;   // state 0 never leaves 0: zero keystream
-  const int n0 = (16 * (int)kScrPhase[S]) % 127;
-  const int plen = len - 4;
-  // payload: dword i = decoded bytes 2+4i .. 5+4i
-  int n = (n0 + 4 * lane) % 127;
-  for (int i = lane; 4 * i < plen; i += 64) {
-    uint32_t v = __builtin_amdgcn_alignbyte(d32[i + 1], d32[i], 2) ^ (scrw[n] & ksm);
-    const int rem = plen - 4 * i;
-    if (rem < 4) v &= (1u << (8 * rem)) - 1u;
-    py32[i] = v;
-    n += 2;                                          // 256 bytes on: 256 = 2 mod 127
-    if (n >= 127) n -= 127;
-  }
-  uint32_t crc;
-  if (plen >= 4) {
-    const int q0 = 32 * lane - (2048 - plen);        // payload index of this lane's first byte
-    uint32_t r = 0;
-    if (q0 + 32 > 0) {
-      const int g = 2 + q0;                          // decoded-byte index of the first byte
-      const int a = g >> 2;
-      const int sh = g & 3;
-      uint32_t w[9];
-#pragma unroll
-      for (int j = 0; j < 9; j++) w[j] = d32[max(a + j, 0)];
-      int m = ((n0 + q0) % 127 + 127) % 127;
-      uint32_t x[8];
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        x[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh) ^ (scrw[m] & ksm);
-        m += 4;
-        if (m >= 127) m -= 127;
-      }
-      if (q0 < 4) {                                  // chunk holds the payload start
-#pragma unroll
+  // grid-stride over packets (one wave per packet at a time): the LDS tables above are
+  // staged once per block, not once per 8 packets
+  for (int p = blockIdx.x * kCrcWaves + wv; p < npkts; p += gridDim.x * kCrcWaves) {
+    int32_t* in = info + 8 * (int64_t)p;
+    const int len = in[2], status = in[5];
+    const int bits = dec_bits[p];
+    if (lane == 0) in[7] = bits;
+    if (status != 0 || bits < (len + 2) * 8 || len < 4) {
+      if (lane == 0) in[4] = 0;
+      continue;
+    }
+    const uint8_t* d = dec + (int64_t)p * kDecStride;
+    const uint32_t* d32 = (const uint32_t*)d;
+    uint32_t* py32 = (uint32_t*)(payload + (int64_t)p * kPayloadStride);
+    const uint32_t S = (uint32_t)d[1] >> 1;           // SERVICE bits 9..15 = scrambler state
+    const uint32_t ksm = S == 0 ? 0u : 0xFFFFFFFFu;   // state 0 never leaves 0: zero keystream
+    const int n0 = (16 * (int)kScrPhase[S]) % 127;
+    const int plen = len - 4;
+    // payload: dword i = decoded bytes 2+4i .. 5+4i
+    int n = (n0 + 4 * lane) % 127;
+    for (int i = lane; 4 * i < plen; i += 64) {
+      uint32_t v = __builtin_amdgcn_alignbyte(d32[i + 1], d32[i], 2) ^ (scrw[n] & ksm);
+      const int rem = plen - 4 * i;
+      if (rem < 4) v &= (1u << (8 * rem)) - 1u;
+      py32[i] = v;
+      n += 2;                                          // 256 bytes on: 256 = 2 mod 127
+      if (n >= 127) n -= 127;
+    }
+    uint32_t crc;
+    if (plen >= 4) {
+      const int q0 = 32 * lane - (2048 - plen);        // payload index of this lane's first byte
+      uint32_t r = 0;
+      if (q0 + 32 > 0) {
+        const int g = 2 + q0;                          // decoded-byte index of the first byte
+        const int a = g >> 2;
+        const int sh = g & 3;
+        uint32_t w[9];
+  #pragma unroll
+        for (int j = 0; j < 9; j++) w[j] = d32[max(a + j, 0)];
+        int m = ((n0 + q0) % 127 + 127) % 127;
+        uint32_t x[8];
+  #pragma unroll
         for (int j = 0; j < 8; j++) {
-          const int qf = q0 + 4 * j;                 // payload index of byte 0 of word j
-          if (qf <= -4) x[j] = 0;
-          else if (qf < 0) x[j] &= 0xFFFFFFFFu << (-8 * qf);   // bytes before the payload
-          if (qf > -4 && qf < 4)                                // complement payload bytes 0..3
-            x[j] ^= qf >= 0 ? 0xFFFFFFFFu >> (8 * qf) : 0xFFFFFFFFu << (-8 * qf);
+          x[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh) ^ (scrw[m] & ksm);
+          m += 4;
+          if (m >= 127) m -= 127;
+        }
+        if (q0 < 4) {                                  // chunk holds the payload start
+  #pragma unroll
+          for (int j = 0; j < 8; j++) {
+            const int qf = q0 + 4 * j;                 // payload index of byte 0 of word j
+            if (qf <= -4) x[j] = 0;
+            else if (qf < 0) x[j] &= 0xFFFFFFFFu << (-8 * qf);   // bytes before the payload
+            if (qf > -4 && qf < 4)                                // complement payload bytes 0..3
+              x[j] ^= qf >= 0 ? 0xFFFFFFFFu >> (8 * qf) : 0xFFFFFFFFu << (-8 * qf);
+          }
+        }
+  #pragma unroll
+        for (int j = 0; j < 8; j++) {
+          r ^= x[j];
+          r = s4[3][r & 0xFFu] ^ s4[2][(r >> 8) & 0xFFu] ^ s4[1][(r >> 16) & 0xFFu] ^ s4[0][r >> 24];
+        }
+        const uint32_t adv = 63u - (uint32_t)lane;     // 32-byte chunks behind this one
+  #pragma unroll
+        for (int k = 0; k < 6; k++) {
+          uint32_t t = 0;
+  #pragma unroll
+          for (int j = 0; j < 8; j++) t ^= shf[k][j * 16 + ((r >> (4 * j)) & 15u)];
+          if ((adv >> k) & 1u) r = t;
         }
       }
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        r ^= x[j];
-        r = s4[3][r & 0xFFu] ^ s4[2][(r >> 8) & 0xFFu] ^ s4[1][(r >> 16) & 0xFFu] ^ s4[0][r >> 24];
-      }
-      const uint32_t adv = 63u - (uint32_t)lane;     // 32-byte chunks behind this one
-#pragma unroll
-      for (int k = 0; k < 6; k++) {
-        uint32_t t = 0;
-#pragma unroll
-        for (int j = 0; j < 8; j++) t ^= shf[k][j * 16 + ((r >> (4 * j)) & 15u)];
-        if ((adv >> k) & 1u) r = t;
-      }
+      crc = ~wave_xor_u32(r);
+    } else {                                           // < 4 payload bytes: the plain register
+      crc = 0xFFFFFFFFu;
+      for (int q = 0; q < plen; q++)
+        crc = s4[0][(crc ^ ((uint32_t)d[2 + q] ^ (scrb[n0 + q] & ksm))) & 0xFFu] ^ (crc >> 8);
+      crc = ~crc;
     }
-    crc = ~wave_xor_u32(r);
-  } else {                                           // < 4 payload bytes: the plain register
-    crc = 0xFFFFFFFFu;
-    for (int q = 0; q < plen; q++)
-      crc = s4[0][(crc ^ ((uint32_t)d[2 + q] ^ (scrb[n0 + q] & ksm))) & 0xFFu] ^ (crc >> 8);
-    crc = ~crc;
-  }
-  if (lane == 0) {
-    uint32_t rx = 0;
-    const int m = (n0 + plen) % 127;
-    for (int k = 0; k < 4; k++) rx |= ((uint32_t)d[2 + plen + k] ^ (scrb[m + k] & ksm)) << (8 * k);
-    in[4] = crc == rx ? 1 : 0;
+    if (lane == 0) {
+      uint32_t rx = 0;
+      const int m = (n0 + plen) % 127;
+      for (int k = 0; k < 4; k++) rx |= ((uint32_t)d[2 + plen + k] ^ (scrb[m + k] & ksm)) << (8 * k);
+      in[4] = crc == rx ? 1 : 0;
+    }
   }
 }
 
