@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round-end evidence: GPU parity suite, default bench (with CPU baseline), rocprof kernel
+# stats + PMC passes of the default bench, then the other BASELINE configs and §8f rows.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -20 gpurun_out/pytest_gpu.log; exit 1; }
+tail -2 gpurun_out/pytest_gpu.log
+timeout -k 10 300 python bench.py > gpurun_out/bench_default.log 2>&1 || exit 1
+tail -1 gpurun_out/bench_default.log | cut -c1-300
+bash scripts/gpu_pmc.sh || exit 1
+for a in "--config 1" "--config 2" "--config 5" "--eq" "--tx"; do
+  f=gpurun_out/bench_$(echo $a | tr -d ' -').log
+  timeout -k 10 300 python bench.py $a --steps 10 > $f 2>&1 || { echo "bench $a failed"; tail -5 $f; exit 1; }
+  tail -1 $f | cut -c1-200
+done
