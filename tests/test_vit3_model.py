@@ -19,6 +19,13 @@ def test_position_map_is_a_bijection():
                     assert V.lane_of(q) == l ^ V.XOR_OF_BIT[bit]
 
 
+def test_dword_selector_identities():
+    """column5 derives dword 1's branch metrics from dword 0's at phases 2 and 4."""
+    S = V.SEL
+    assert all(S[2, l, 0] == S[2, l, 1] for l in range(16))
+    assert all((S[4, l, 0] ^ S[4, l, 1]) == ((4 ^ 12) | ((4 ^ 12) << 16)) for l in range(16))
+
+
 @pytest.mark.parametrize("v4", [False, True, 5])
 @pytest.mark.parametrize("idx", range(0, 48, 5))
 def test_model_matches_reference_frames(golden, idx, v4):

@@ -189,15 +189,26 @@ __device__ __forceinline__ void column5(uint32_t& M0, uint32_t& M1, uint32_t P, 
   constexpr uint32_t mk = 2u << KPH;
   constexpr uint32_t Kc = KIND == 0 ? 28u : 14u;
   constexpr uint32_t C = KPH == 7 ? ((Kc + 1u) << 8) * 0x00010001u : ((Kc << 8) | mk) * 0x00010001u;
+  // Dword 1 holds dword 0's positions with position bit 1 set, i.e. state bit (1 + PH) % 6
+  // flipped: at PH 2 that is state bit 3, which changes neither expected bit nor the
+  // marker (BX1 = BX0); at PH 4 it is bit 5, the marker only (BX1 = BX0 ^ marker bits).
+  // tests/test_vit3_model.py checks both selector identities.
+  constexpr uint32_t mbits = KPH == 7 ? 0x01000100u : mk * 0x00010001u;
   uint32_t BX0, BX1;
   if constexpr (KPH == 7) {
     BX0 = __builtin_amdgcn_perm(0x80808080u, P, K.sel[PH][0]);
-    BX1 = __builtin_amdgcn_perm(0x80808080u, P, K.sel[PH][1]);
     BX0 += BX0 & 0x00FF00FFu;
-    BX1 += BX1 & 0x00FF00FFu;
+    if constexpr (PH == 2) BX1 = BX0;
+    else if constexpr (PH == 4) BX1 = BX0 ^ mbits;
+    else {
+      BX1 = __builtin_amdgcn_perm(0x80808080u, P, K.sel[PH][1]);
+      BX1 += BX1 & 0x00FF00FFu;
+    }
   } else {
     BX0 = __builtin_amdgcn_perm((mk & 0xFFu) * 0x01010101u, P, K.sel[PH][0]);
-    BX1 = __builtin_amdgcn_perm((mk & 0xFFu) * 0x01010101u, P, K.sel[PH][1]);
+    if constexpr (PH == 2) BX1 = BX0;
+    else if constexpr (PH == 4) BX1 = BX0 ^ mbits;
+    else BX1 = __builtin_amdgcn_perm((mk & 0xFFu) * 0x01010101u, P, K.sel[PH][1]);
   }
   const uint32_t BY0 = C - BX0, BY1 = C - BX1;
   const uint32_t X0 = T0 + BX0, X1 = T1 + BX1;
