@@ -101,24 +101,55 @@ struct RingLds {
   __device__ __forceinline__ uint64_t operator()(uint32_t t) const { return r[t & (kRing - 1)]; }
 };
 
-// Viterbi_sig11: 24 full steps on 48 soft values held as 12 dwords in lanes 0..11 of `dw`.
-// Returns (in lane j) traceback byte j of the 3 output bytes (before the >>6 of :191).
-__device__ __forceinline__ uint32_t sig11_bytes(uint32_t dw, int lane, uint64_t* ring) {
+// Wave minimum by DPP inside each 16-lane row (xor 1, xor 2, half-row and row mirrors) and
+// four readlanes across rows: no ds_bpermute (the LDS pipe is this kernel's bottleneck).
+template <typename T>
+__device__ __forceinline__ T wave_min_dpp(T v) {
+  v = min(v, (T)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
+  v = min(v, (T)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
+  v = min(v, (T)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));
+  v = min(v, (T)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false));
+  const T a = (T)__builtin_amdgcn_readlane((int)v, 0), b = (T)__builtin_amdgcn_readlane((int)v, 16);
+  const T c = (T)__builtin_amdgcn_readlane((int)v, 32), d = (T)__builtin_amdgcn_readlane((int)v, 48);
+  return min(min(a, b), min(c, d));
+}
+
+// Viterbi_sig11 (viterbicore.hpp:272-315): 24 full steps on 48 soft values held as 12 dwords
+// in lanes 0..11 of `dw`, normalize every 8 steps and once more at the end, traceback of 24
+// bits with lookahead 0 (viterbicore.hpp:170-239).  The 24 survivor words (ballots of the
+// metric LSBs) stay in SGPRs and the traceback runs on the scalar unit.  Returns the three
+// traceback bytes, byte 0 lowest (before the brick's >> 6 at sora_ext_viterbi.cpp:191).
+__device__ __forceinline__ uint32_t sig11_word(uint32_t dw, int lane) {
   const VitLane L = vit_lane(lane);
   uint32_t m = lane == 0 ? 0u : 48u;
-  if (lane == 0) ring[0] = 0;
+  uint64_t surv[24];
+  surv[0] = 0;                                         // column 0: no markers
 #pragma unroll
   for (int t = 1; t <= 24; t++) {
     const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)dw, (2 * t - 2) >> 2);
     const int sh = ((2 * t - 2) & 3) * 8;
     const int a = (word >> sh) & 0xFF, b = (word >> (sh + 8)) & 0xFF;
     m = acs<3>(m, a, b, L);
-    if ((t & 7) == 0) m = vit_normalize(m);
-    const uint64_t w = __ballot((m & 1u) != 0);
-    if (lane == 0) ring[t] = w;
+    if ((t & 7) == 0) m -= wave_min_dpp<uint32_t>(m) & 0xFEu;
+    if (t < 24) surv[t] = __ballot((m & 1u) != 0);
   }
-  m = vit_normalize(m);
-  return vit_traceback(m, 24u, 24u, 0u, lane, RingLds{ring});
+  m -= wave_min_dpp<uint32_t>(m) & 0xFEu;
+  const int key = wave_min_dpp<int>((int)(int16_t)(uint16_t)((m << 8) | ((uint32_t)lane << 2)));
+  uint32_t i = (uint32_t)__builtin_amdgcn_readfirstlane((key >> 2) & 0x7F);
+  uint32_t word = 0;
+#pragma unroll
+  for (int byte = 2; byte >= 0; byte--) {
+    uint32_t oc = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const int t = 8 * byte + 7 - j;                  // column read by this step
+      oc = (oc << 1) | ((i >> 6) & 1u);
+      i = (i >> 1) & 0x3Fu;
+      i |= (uint32_t)((surv[t] >> i) & 1u) << 6;
+    }
+    word |= oc << (8 * byte);
+  }
+  return word;
 }
 
 __device__ __forceinline__ int ncbps_of(int mod) { return mod == 0 ? 48 : mod == 1 ? 96 : mod == 2 ? 192 : 288; }
@@ -134,16 +165,11 @@ __device__ __forceinline__ int ndbps_of(int mod, int coding) {
 __global__ __launch_bounds__(256) void k_signal_vit(const uint32_t* __restrict__ sig_soft, const int32_t* __restrict__ nsym,
                                                     int npkts, int32_t* __restrict__ vparams,
                                                     int32_t* __restrict__ info) {
-  __shared__ uint64_t ring_all[4][32];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int p = blockIdx.x * 4 + wv;
   if (p >= npkts) return;
   const uint32_t dw = lane < 12 ? sig_soft[(int64_t)p * 12 + lane] : 0u;
-  const uint32_t byte = sig11_bytes(dw, lane, ring_all[wv]);
-  const uint32_t b0 = __builtin_amdgcn_readlane((int)byte, 0);
-  const uint32_t b1 = __builtin_amdgcn_readlane((int)byte, 1);
-  const uint32_t b2 = __builtin_amdgcn_readlane((int)byte, 2);
-  const uint32_t hb = ((b0 | (b1 << 8) | (b2 << 16)) >> 6) & 0x3FFFFu;   // bits 18..23 := 0
+  const uint32_t hb = (sig11_word(dw, lane) >> 6) & 0x3FFFFu;   // bits 18..23 := 0
   // parsePLCPHeader.blk:124-158 RATE nibble (bit k of the nibble = hdata[k])
   int mod = 0, cod = 0;
   switch (hb & 0xF) {
@@ -523,13 +549,12 @@ __global__ void k_viterbi_stream(VitStream* st, const uint8_t* __restrict__ sp, 
 }
 // Viterbi_sig11 for a batch: 3 traceback bytes per packet (before the brick's >>6).
 __global__ __launch_bounds__(256) void k_sig_bytes(const uint32_t* __restrict__ sig_soft, int npkts, uint8_t* __restrict__ out3) {
-  __shared__ uint64_t ring_all[4][32];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int p = blockIdx.x * 4 + wv;
   if (p >= npkts) return;
   const uint32_t dw = lane < 12 ? sig_soft[(int64_t)p * 12 + lane] : 0u;
-  const uint32_t byte = sig11_bytes(dw, lane, ring_all[wv]);
-  if (lane < 3) out3[(int64_t)p * 3 + lane] = (uint8_t)byte;
+  const uint32_t word = sig11_word(dw, lane);
+  if (lane < 3) out3[(int64_t)p * 3 + lane] = (uint8_t)(word >> (8 * lane));
 }
 // __ext_v_shift_right_complex16 (sora_ext_lib.cpp:1979-1995): the first len/4*4 complex
 // values use srai_epi16 (arithmetic); the tail uses unum16 >> shift (logical).
