@@ -450,10 +450,10 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
   }
   if (ev) ZRX_CHECK(hipEventRecord(ev[0], s));
   if (chan)
-    k_signal_fft<true><<<blocks(npkts, 256), 256, 0, s>>>((const uint4*)d_sym, d_sym_off, d_nsym, npkts,
+    k_signal_fft<true><<<blocks(npkts, 64), 64, 0, s>>>((const uint4*)d_sym, d_sym_off, d_nsym, npkts,
                                                           (uint4*)c->sig_soft, chan, T);
   else
-    k_signal_fft<false><<<blocks(npkts, 256), 256, 0, s>>>((const uint4*)d_sym, d_sym_off, d_nsym, npkts,
+    k_signal_fft<false><<<blocks(npkts, 64), 64, 0, s>>>((const uint4*)d_sym, d_sym_off, d_nsym, npkts,
                                                            (uint4*)c->sig_soft, chan, T);
   if (ev) ZRX_CHECK(hipEventRecord(ev[1], s));
   k_signal_vit<<<blocks(npkts, 4), 256, 0, s>>>(c->sig_soft, d_nsym, npkts, c->vparams, d_info);
