@@ -156,6 +156,42 @@ __device__ __forceinline__ uint32_t crc32_bytes(const uint8_t* __restrict__ p, i
   return ~c;
 }
 
+// The same CRC by the whole wave (n <= 2048): lane l takes the 32-byte chunk l of the n
+// bytes right-aligned in a 2048-byte frame (chunks before the data are zero and leave a
+// zero-initialised register at zero; the all-ones init is folded in by complementing the
+// first 4 data bytes), runs slicing-by-4 (kCrcS4) over it, advances the result past the
+// 63 - l chunks behind it with the 32·2^k-zero-byte maps (kCrcShift), and the wave XORs the
+// partial registers -- the k_descramble_crc scheme without the descrambler.
+__device__ __forceinline__ uint32_t crc32_wave(const uint8_t* __restrict__ p, int n, int lane) {
+  if (n < 4) return (uint32_t)__builtin_amdgcn_readfirstlane((int)crc32_bytes(p, n));
+  const int q0 = 32 * lane - (2048 - n);                // data index of this lane's first byte
+  uint32_t r = 0;
+  if (q0 + 32 > 0) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const int q = q0 + 4 * j + b;
+        uint32_t v = q >= 0 ? (uint32_t)p[max(q, 0)] : 0u;
+        if (q >= 0 && q < 4) v ^= 0xFFu;
+        x |= v << (8 * b);
+      }
+      r ^= x;
+      r = kCrcS4[3][r & 0xFFu] ^ kCrcS4[2][(r >> 8) & 0xFFu] ^ kCrcS4[1][(r >> 16) & 0xFFu] ^ kCrcS4[0][r >> 24];
+    }
+    const uint32_t adv = 63u - (uint32_t)lane;
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      uint32_t t = 0;
+#pragma unroll
+      for (int j = 0; j < 8; j++) t ^= kCrcShift[k][j * 16 + ((r >> (4 * j)) & 15u)];
+      if ((adv >> k) & 1u) r = t;
+    }
+  }
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)~wave_xor_u32(r));
+}
+
 // in: per packet 3 PLCP header bytes (emitHeader, parsePLCPHeader.blk:215-221) then len-4
 // payload bytes; out: 640 + 160 * (1 + nsym) complex16 samples at out_off[p].
 __global__ __launch_bounds__(64) void k_tx(const uint8_t* __restrict__ in, const int64_t* __restrict__ in_off,
@@ -186,7 +222,7 @@ __global__ __launch_bounds__(64) void k_tx(const uint8_t* __restrict__ in, const
   const int nc = mod == 0 ? 48 : mod == 1 ? 96 : mod == 2 ? 192 : 288;
   const int nd = cod == 0 ? nc / 2 : cod == 1 ? nc * 2 / 3 : nc * 3 / 4;
   const int nsym = (16 + 8 * plen + 32 + 6 + nd - 1) / nd;
-  const uint32_t crc = (uint32_t)__builtin_amdgcn_readfirstlane((int)(lane == 0 ? crc32_bytes(src + 3, plen) : 0u));
+  const uint32_t crc = crc32_wave(src + 3, plen, lane);
   uint32_t* dst = out + out_off[p];
   if (lane == 0) nsamp[p] = 640 + 160 * (1 + nsym);
   for (int i = lane; i < 640; i += 64) dst[i] = preamble[i];
