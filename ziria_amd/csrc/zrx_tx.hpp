@@ -111,8 +111,9 @@ struct Stream {
     return c < 32 ? (crc >> c) & 1u : 0u;
   }
   __device__ __forceinline__ uint32_t bit(int b) const {
-    const int m = b % 127;
-    return raw(b) ^ ((kTxKey[m >> 5] >> (m & 31)) & 1u);
+    const int m = b % 127, w = m >> 5;                 // keystream word by selects, not a load
+    const uint32_t key = w == 0 ? kTxKey[0] : w == 1 ? kTxKey[1] : w == 2 ? kTxKey[2] : kTxKey[3];
+    return raw(b) ^ ((key >> (m & 31)) & 1u);
   }
 };
 
@@ -199,6 +200,7 @@ __global__ __launch_bounds__(64) void k_tx(const uint8_t* __restrict__ in, const
                                            uint32_t* __restrict__ out, const int64_t* __restrict__ out_off,
                                            int32_t* __restrict__ nsamp) {
   __shared__ uint8_t lds[64 * 288];
+  __shared__ uint8_t pay[2048];                           // the payload, read bit by bit below
   const int lane = threadIdx.x;
   const int p = blockIdx.x;
   if (p >= npkts) return;
@@ -226,7 +228,9 @@ __global__ __launch_bounds__(64) void k_tx(const uint8_t* __restrict__ in, const
   uint32_t* dst = out + out_off[p];
   if (lane == 0) nsamp[p] = 640 + 160 * (1 + nsym);
   for (int i = lane; i < 640; i += 64) dst[i] = preamble[i];
-  const Stream S{src + 3, plen, crc};
+  for (int i = lane; i < plen; i += 64) pay[i] = src[3 + i];
+  __syncthreads();
+  const Stream S{pay, plen, crc};
   uint8_t* cb = lds + lane * 288;
   for (int k = lane; k < 1 + nsym; k += 64) {
     s2 sub[48];
