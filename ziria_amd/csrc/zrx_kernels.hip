@@ -215,11 +215,8 @@ __device__ __forceinline__ void data_fft_packet(const uint4* __restrict__ sym0, 
     load_symbol(sym0 + (int64_t)k * 16, x);
     fft64_inplace(x);
     if constexpr (EQ) equalize_data_bins(x, [cp](int b) { return as_s2(cp[b]); }, k + 1, T);
-    uint32_t w[NC / 4];
-    demap_deinterleave<MOD>(x, lut, w);
     uint4* dst = dst0 + (int64_t)k * (NC / 16);
-#pragma unroll
-    for (int q = 0; q < NC / 16; q++) dst[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    demap_deinterleave_st<MOD>(x, lut, [dst](int q, uint4 v) { dst[q] = v; });
   }
 }
 template <bool EQ>
