@@ -36,6 +36,7 @@ sys.path.insert(0, ROOT)
 
 from ziria_amd import node, txgen  # noqa: E402
 from ziria_amd._lib import lib as zlib  # noqa: E402
+from ziria_amd.build import source_hash  # noqa: E402
 from ziria_amd.engine import RxEngine  # noqa: E402
 
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz = 78.6
@@ -45,14 +46,15 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
 
 
 def traffic_for(kernel, npkts):
-    """HBM bytes per launch of `kernel` from the committed PMC summary (same workload)."""
+    """HBM bytes per launch of `kernel` from the committed PMC summary of the same workload
+    and the same kernel sources (csrc_sha256, ziria_amd.build.source_hash); None otherwise."""
     try:
         s = json.load(open(PMC_SUMMARY))
         k = s["kernels"][kernel]
-        if int(s.get("npkts", -1)) != npkts:
+        if int(s.get("npkts", -1)) != npkts or s.get("csrc_sha256") != source_hash():
             return None
         return k.get("hbm_bytes_per_launch")
-    except (OSError, KeyError, ValueError):
+    except (OSError, KeyError, ValueError, TypeError):
         return None
 
 
@@ -61,7 +63,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--npkts", type=int, default=16384)
+    ap.add_argument("--npkts", type=int, default=16384, help="packets per GPU (config 3: 16384)")
+    ap.add_argument("--total", type=int, default=0,
+                    help="global packet count split over the ranks (default npkts x N, i.e. weak scaling)")
     ap.add_argument("--payload", type=int, default=1500)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall time budget of the CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
@@ -88,63 +92,51 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    def barrier():
-        if world > 1:
-            dist.barrier()
-
     # ---------------------------------------------------------------- workload (HBM-resident)
-    b = txgen.make_batch(args.npkts, mod=3, coding=2, payload_len=args.payload,
-                         seed=0x5EED + 7919 * rank, device=dev, channel=args.eq,
-                         sigma=2.0 if args.eq else 4.0)
-    chan = b.get("chan")
-    n, S = args.npkts, b["max_nsym"]
+    # One global batch (BASELINE config 4): packet i depends only on (seed, i), each rank
+    # builds and decodes its contiguous shard, rank 0 checks every gathered packet.
+    total = args.total if args.total else args.npkts * world
+    sigma = 2.0 if args.eq else 4.0
     eng = RxEngine(local)
-    eng.reserve(n, S)
-    payload = torch.zeros((n, 4096), dtype=torch.uint8, device=dev)
-    info = torch.zeros((n, 8), dtype=torch.int32, device=dev)
+    state = {}
 
-    def step():
-        eng.rx(b["sym"], b["sym_off"], b["nsym"], S, payload, info, chan=chan)
+    def make_shard(lo, hi):
+        b = txgen.make_batch_range(lo, hi, mod=3, coding=2, payload_len=args.payload, sigma=sigma, seed=0x5EED,
+                                   device=dev, channel=args.eq)
+        n, S = hi - lo, b["max_nsym"]
+        eng.reserve(max(n, 1), S)
+        b["out_payload"] = torch.zeros((n, 4096), dtype=torch.uint8, device=dev)
+        b["out_info"] = torch.zeros((n, 8), dtype=torch.int32, device=dev)
+        state["b"] = b
+        return b
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    eng.enable_timing(True)                       # stage events on the engine's stream, every step
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    barrier()
-    t1 = time.perf_counter()
+    def step(b):
+        eng.rx(b["sym"], b["sym_off"], b["nsym"], b["max_nsym"], b["out_payload"], b["out_info"], chan=b.get("chan"))
+
+    res = node.run_sharded(total, make_shard, step, lambda b: (b["out_payload"], b["out_info"]),
+                           lambda lo, hi: txgen.payloads_range(lo, hi, args.payload, seed=0x5EED),
+                           args.steps, args.warmup, args.payload, device=dev, crc_ok_only=args.eq,
+                           on_timed=lambda on: eng.enable_timing(on) if on else None)
     stage = eng.stage_ms()                        # averages over the K timed steps
     eng.enable_timing(False)
-    elapsed = node.max_over_ranks(t1 - t0, device=dev)
+    b = state["b"]
+    n, S = res["hi"] - res["lo"], b["max_nsym"]
+    elapsed = res["elapsed"]
 
-    # ---------------------------------------------------------------- bit-exact self-check + gather
-    ok, bits, match = node.counts(info, payload=payload, expected=b["payload"], crc_ok_only=args.eq)
-    torch.cuda.synchronize()
-    tg = time.perf_counter()
-    ok_all, bits_all, match_all, _ = node.combine(ok, bits, match, payload[:, :args.payload].contiguous(),
-                                                  device=dev)
-    torch.cuda.synchronize()
-    gather_ms = (time.perf_counter() - tg) * 1e3 if world > 1 else 0.0
-
-    decoded_bits = n * (args.payload + 4 + 2) * 8          # Viterbi output bits per launch
+    decoded_bits = n * (args.payload + 4 + 2) * 8          # Viterbi output bits per launch (this rank)
     vit_ms = stage["data_viterbi"]
     achieved_tops = OPS_PER_DECODED_BIT * decoded_bits / (vit_ms * 1e-3) / 1e12
     nsym_data = S - 1
     fft_bytes = n * nsym_data * (256 + 288)                # complex16 symbol in + 64-QAM soft out
     fft_gbs = fft_bytes / (stage["data_fft_demap"] * 1e-3) / 1e9
 
-    value = bits_all * args.steps / elapsed / 1e6          # CRC-checked payload bits, all ranks
+    value = res["bits"] * args.steps / elapsed / 1e6       # CRC-checked payload bits, all ranks
     ms_per_step = elapsed / args.steps * 1e3
 
     # ---------------------------------------------------------------- CPU baseline (rank 0, N=1)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(b, args.payload, args.cpu_seconds, chan)
+        cpu = cpu_baseline(b, args.payload, args.cpu_seconds, b.get("chan"))
 
     if rank == 0:
         line = {
@@ -156,18 +148,22 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if not args.total else "strong",
             "vs_baseline": None,
             "dtype": "int16+u8",
-            "data": ("synthetic (txgen: random payloads, TX restated from transmitter.blk, "
+            "data": ("synthetic (txgen.make_batch_range: random payloads, TX restated from transmitter.blk, "
                      + ("3-tap channel + phase drift, AWGN sigma=2)" if args.eq else "AWGN sigma=4)")),
-            "config": {"workload": f"config3{'+eq' if args.eq else ''}: {n} packets/GPU x {args.payload} B payload "
+            "config": {"workload": f"config{'3+eq' if args.eq else ('4' if world > 1 else '3')}: {total} packets "
+                                   f"({n} per GPU, contiguous shards) x {args.payload} B payload "
                                    f"@ 54 Mbps (64-QAM r3/4), {S} CP-removed complex16 OFDM symbols each, "
                                    "time-domain input resident in HBM"
                                    + (", FFT >>> ChannelEqualization >>> PilotTrack >>> GetData" if args.eq else ""),
-                       "packets_per_gpu": n, "payload_bytes": args.payload, "symbols_per_packet": S,
-                       "parallelism": f"packet-sharded x{world}"},
-            "bit_exact_check": {"crc_pass": ok_all, "packets": n * world, "payload_match": match_all == world},
+                       "packets_total": total, "packets_per_gpu": n, "payload_bytes": args.payload,
+                       "symbols_per_packet": S, "parallelism": f"packet-sharded x{world}"},
+            "bit_exact_check": {"crc_pass": res["ok"], "packets": res["packets"],
+                                "payload_match": res["payload_match"],
+                                "mismatched_packets": res["mismatched_packets"],
+                                "checked_on": "rank 0, every gathered packet vs its transmitted payload"},
             "stage_ms": {k: round(v, 4) for k, v in stage.items()},
             "roofline": {"kernel": "k_viterbi3 (data Viterbi)", "bound": "valu",
                          "achieved": round(achieved_tops, 3), "peak": round(VALU_PEAK_TOPS, 1),
@@ -179,7 +175,7 @@ def main():
                              "frac": round(fft_gbs / HBM_PEAK_GBS, 4),
                              "traffic": None if args.eq else traffic_for("k_data_fft", n),
                              "units": f"544 B per data symbol x {n * nsym_data} symbols/launch"},
-            "gather_ms": round(gather_ms, 3),
+            "gather_ms": round(res["gather_s"] * 1e3, 3),
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
@@ -402,17 +398,45 @@ def bench_tx(args):
     }), flush=True)
 
 
+def host_cpus():
+    """(threads to use, description) for the CPU baseline: every core this process may run
+    on (sched_getaffinity), capped by the cgroup CPU quota (cpu.max) and OMP_NUM_THREADS
+    when those are set (the GPU box gives one GPU's job a 16-core share), plus the CPU
+    model string."""
+    nproc = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    omp = int(os.environ["OMP_NUM_THREADS"]) if os.environ.get("OMP_NUM_THREADS", "").isdigit() else None
+    threads = min(x for x in (aff, quota, omp) if x)
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return threads, {"nproc": nproc, "affinity": aff, "cgroup_cpu_quota": quota, "omp_num_threads": omp,
+                     "cpu_model": model}
+
+
 def cpu_baseline(b, payload_len, seconds, chan=None):
-    """The oracle (scalar C restatement, "port") on the host cores this process may use,
-    packet-parallel with pthreads, over chunks of the same packets until `seconds` of wall
-    time have passed."""
+    """The oracle (scalar C restatement, "port") on every host core this process is allowed
+    (host_cpus), packet-parallel with pthreads, over chunks of the same packets until
+    `seconds` of wall time have passed."""
     from oracle import oracle as O
-    threads = min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count() or 1)
+    threads, host = host_cpus()
     sym = b["sym"].cpu().numpy()
     off_all = b["sym_off"].cpu().numpy()
     ns_all = b["nsym"].cpu().numpy()
     ch_all = chan.cpu().numpy() if chan is not None else None
-    chunk = 1024
+    chunk = max(1024, 64 * threads)
     done = ok = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
@@ -427,7 +451,9 @@ def cpu_baseline(b, payload_len, seconds, chan=None):
     dt = time.perf_counter() - t0
     bits = ok * payload_len * 8
     return {"value": round(bits / dt / 1e6, 2), "unit": "Mbit/s", "cores": threads, "kind": "port",
-            "sample": f"{done} packets of the same batch ({ok} CRC-ok), {dt:.1f} s wall on {threads} threads"}
+            "per_core": round(bits / dt / 1e6 / threads, 2), "host": host,
+            "sample": f"{done} packets of the same batch ({ok} CRC-ok), {dt:.1f} s wall on {threads} threads "
+                      "(scalar C oracle; the reference SSE2 bricks run 41-73 Mbit/s per core, SURVEY.md §6)"}
 
 
 if __name__ == "__main__":

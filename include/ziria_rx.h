@@ -130,6 +130,7 @@ int32_t __ext_wifi_tx_batch(unsigned char* in, int inlen, int32_t* pkt_in_off, i
 #define ZRX_PKT_OK 0
 #define ZRX_PKT_HDR_ERR 1      /* PLCP header parity/tail/length error: no payload (as the reference) */
 #define ZRX_PKT_TRUNCATED 2    /* fewer symbols than the header requires */
+#define ZRX_PKT_OVERSIZE 3     /* header needs more symbols than the reserved workspace holds (zrx_reserve) */
 
 typedef struct zrx_ctx zrx_ctx;
 
@@ -159,7 +160,10 @@ int zrx_viterbi_dev(zrx_ctx* ctx, const int8_t* d_soft, const int64_t* d_soft_of
                     int32_t* d_out_bits);
 
 /* Full chain; d_sym_off: int64 symbol index of each packet's SIGNAL symbol; d_nsym: int32
- * symbols available per packet; max_nsym: bound on d_nsym (grid sizing).  d_payload holds
+ * symbols available per packet; max_nsym: the largest d_nsym, which must fit the reserved
+ * workspace (zrx_reserve).  The device never writes past a packet's workspace slot: a packet
+ * whose PLCP header needs more symbols than the workspace holds (possible only when d_nsym
+ * exceeds the reservation) gets status ZRX_PKT_OVERSIZE and no payload.  d_payload holds
  * npkts*4096 bytes, d_info npkts*8 int32 (layout as __ext_wifi_rx_batch). */
 int zrx_rx_dev(zrx_ctx* ctx, const struct complex16* d_sym, const int64_t* d_sym_off,
                const int32_t* d_nsym, int npkts, int max_nsym, uint8_t* d_payload,

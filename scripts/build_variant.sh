@@ -9,6 +9,6 @@ TMP=$(mktemp -d)
 trap 'rm -rf "$TMP"' EXIT
 git -C "$ROOT" archive "$REV" ziria_amd/csrc include | tar -x -C "$TMP"
 python3 "$TMP/ziria_amd/csrc/gen_tables.py"
-hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -o "$ROOT/ziria_amd/_lib/libziria_rx.$NAME.so" \
+hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DZRX_EXPERIMENTS -o "$ROOT/ziria_amd/_lib/libziria_rx.$NAME.so" \
   "$TMP/ziria_amd/csrc/zrx_api.hip"
 echo "$ROOT/ziria_amd/_lib/libziria_rx.$NAME.so"

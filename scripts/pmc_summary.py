@@ -62,8 +62,17 @@ def main(root):
         for line in open(lg):
             if line.startswith("{"):
                 npkts = json.loads(line)["config"]["packets_per_gpu"]
-    res = {"npkts": npkts, "source": "rocprofv3 --pmc, one timed step + one warmup of bench.py; "
-                                      "durations from the kernel-trace run of the default bench",
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from ziria_amd.build import source_hash
+    import subprocess
+    try:
+        rev = subprocess.check_output(["git", "rev-parse", "--short", "HEAD"], text=True,
+                                      stderr=subprocess.DEVNULL).strip()
+    except (OSError, subprocess.CalledProcessError):
+        rev = None
+    res = {"npkts": npkts, "csrc_sha256": source_hash(), "git_head": rev,
+           "source": "rocprofv3 --pmc, one timed step + one warmup of bench.py; "
+                     "durations from the kernel-trace run of the default bench",
            "kernels": {}}
     for k, cs in counters.items():
         if not k.startswith("k_"):

@@ -117,6 +117,26 @@ def test_viterbi_per_call_stream(golden):
         assert (got == g["vit_out"][oo[i]:oo[i + 1]]).all(), f"case {(cr, fl, noise)}"
 
 
+def test_viterbi_per_call_depths_vs_oracle(oracle):
+    """Per-call externals with depths other than 256 and call sizes other than 48, call by
+    call against the oracle (itself pinned on these cases by test_oracle_vs_ref.py).  Most
+    calls emit nothing and are queued on the host; the others run the queue on the GPU."""
+    from tests.golden import synth
+    from tests.test_oracle_vs_ref import _per_call_cases
+    for cr, fl, noise, depth, call, seed in _per_call_cases():
+        s = synth.viterbi_soft(cr, fl, noise, seed=seed)
+        Z.viterbi_brick_init_fast(fl, cr, depth)
+        d = oracle.Viterbi()
+        d.init(fl, cr, depth)
+        for k in range(0, s.size, call):
+            c = np.ascontiguousarray(s[k:k + call])
+            if c.size % 12:
+                break
+            nb, got = Z.viterbi_brick_decode_fast(c)
+            exp = d.decode(c)
+            assert nb == 8 * exp.size and (got == exp).all(), (cr, fl, depth, call, k)
+
+
 def test_viterbi_batch_random_vs_oracle(oracle):
     rng = np.random.default_rng(77)
     softs, offs, fls, crs = [], [0], [], []
@@ -229,6 +249,30 @@ def test_chain_truncated_and_bad_header(engine, oracle):
     assert (info[2, 0], info[2, 1], info[2, 2], info[2, 3]) == (r2["modulation"], r2["coding"], r2["len"], r2["err"])
     for i in (0, 3, 4, 5, 6, 7):
         assert info[i, 4] == 1
+
+
+def test_chain_nsym_beyond_reservation():
+    """d_nsym larger than the reserved workspace: packets whose header needs more
+    symbols than a soft slot holds get ZRX_PKT_OVERSIZE and nothing is written past their
+    slot; the short packets around them still decode exactly."""
+    short = txgen.make_batch(3, payload_len=100, seed=21, device="cuda")       # 5 symbols each
+    long = txgen.make_batch(2, payload_len=1500, seed=22, device="cuda")       # 57 symbols each
+    Ss, Sl = short["max_nsym"], long["max_nsym"]
+    sym = torch.cat([short["sym"][:Ss], long["sym"][:Sl], short["sym"][Ss:2 * Ss], long["sym"][Sl:],
+                     short["sym"][2 * Ss:]])
+    nsym = torch.tensor([Ss, Sl, Ss, Sl, Ss], dtype=torch.int32, device="cuda")
+    off = torch.cumsum(torch.cat([torch.zeros(1, dtype=torch.int64, device="cuda"), nsym.to(torch.int64)]), 0)[:5]
+    e = RxEngine(0)
+    e.reserve(5, 12)                                     # room for 11 data symbols per packet
+    pay, info = e.rx(sym.contiguous(), off.contiguous(), nsym, 12)
+    pay, info = pay.cpu().numpy(), info.cpu().numpy()
+    e.close()
+    for i, j in ((0, 0), (2, 1), (4, 2)):
+        assert info[i, 5] == 0 and info[i, 4] == 1
+        assert (pay[i, :100] == short["payload"][j]).all()
+    for i in (1, 3):
+        assert info[i, 5] == 3 and info[i, 4] == 0 and info[i, 2] == 1504
+        assert (pay[i] == 0).all()
 
 
 def test_chain_large_batch_properties(engine):

@@ -1,6 +1,8 @@
 """The N>1 path of bench.py (ziria_amd/node.py) on CPU: world_size-2 gloo process groups
-stand in for RCCL.  Per-rank decode results are synthetic here (the decode itself is
-GPU-only); what is checked is the sharding and the final combine of counts and payloads."""
+stand in for RCCL.  Per-rank decode results come from a stub decoder here (the decode itself
+is GPU-only); what is checked is the sharding, the timed loop, the final combine of counts
+and the gather + per-packet check of payloads, including unequal shards.  run_sharded is
+the function bench.py's main() calls, so this is the driver's 1/2/4/8-GPU code path."""
 import os
 import socket
 
@@ -59,14 +61,13 @@ def _worker(rank, world, port, npkts, out):
         elapsed = node.max_over_ranks(0.5 + rank)
         o, b, m, g = node.combine(ok, bits, match, pay)
         if rank == 0:
-            out.put((o, b, m, elapsed, torch.cat(g).tolist()))
+            out.put((o, b, m, elapsed, g.tolist()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_combine_over_gloo(world):
-    npkts = 10                                   # equal shards (gather needs equal shapes)
+@pytest.mark.parametrize("world,npkts", [(2, 10), (2, 11), (3, 7)])
+def test_combine_over_gloo(world, npkts):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -83,3 +84,70 @@ def test_combine_over_gloo(world):
     assert elapsed == 0.5 + (world - 1)
     exp = ((torch.arange(npkts).unsqueeze(1) * 7 + torch.arange(24)) % 251).to(torch.uint8)
     assert gathered == exp.tolist()
+
+
+L = 24
+
+
+def _payload(lo, hi):
+    return ((torch.arange(lo, hi).unsqueeze(1) * 7 + torch.arange(L)) % 251).to(torch.uint8).numpy()
+
+
+def _bench_worker(rank, world, port, total, corrupt, out):
+    """bench.py main() with the engine replaced by a stub that 'decodes' by copying the
+    transmitted payload (and, with corrupt, flips one byte of global packet 5)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        calls = {"step": 0}
+
+        def make_shard(lo, hi):
+            return {"lo": lo, "hi": hi, "pay": torch.zeros((hi - lo, 64), dtype=torch.uint8),
+                    "info": torch.zeros((hi - lo, 8), dtype=torch.int32)}
+
+        def step(sh):
+            calls["step"] += 1
+            sh["pay"][:, :L] = torch.from_numpy(_payload(sh["lo"], sh["hi"]))
+            if corrupt and sh["lo"] <= 5 < sh["hi"]:
+                sh["pay"][5 - sh["lo"], 3] ^= 1
+            sh["info"][:, 2] = L + 4
+            sh["info"][:, 4] = 1
+
+        timed = []
+        res = node.run_sharded(total, make_shard, step, lambda sh: (sh["pay"], sh["info"]), _payload,
+                               steps=3, warmup=2, payload_len=L, on_timed=timed.append)
+        out.put((rank, res["lo"], res["hi"], calls["step"], timed, res["ok"], res["bits"],
+                 res.get("packets"), res.get("payload_match"), res.get("mismatched_packets")))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,total,corrupt", [(2, 11, False), (2, 16, False), (2, 11, True), (3, 11, False)])
+def test_run_sharded_over_gloo(world, total, corrupt):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, total, corrupt, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ranges = [(g[1], g[2]) for g in got]
+    assert ranges == [node.shard_range(total, world, r) for r in range(world)]
+    for g in got:
+        assert g[3] == 5 and g[4] == [True, False]          # 2 warmup + 3 timed steps, timers on/off
+        assert g[5] == total and g[6] == total * L * 8      # summed over ranks
+    r0 = got[0]
+    assert r0[7] == total
+    assert r0[8] is (not corrupt)
+    assert r0[9] == (1 if corrupt else 0)
+
+
+def test_run_sharded_single_process():
+    res = node.run_sharded(5, lambda lo, hi: {"p": torch.from_numpy(_payload(lo, hi)),
+                                              "i": torch.ones((hi - lo, 8), dtype=torch.int32) * 0 + torch.tensor([0, 0, L + 4, 0, 1, 0, 0, 0], dtype=torch.int32)},
+                           lambda sh: None, lambda sh: (sh["p"], sh["i"]), _payload, steps=1, warmup=0, payload_len=L)
+    assert (res["lo"], res["hi"], res["ok"], res["packets"], res["payload_match"]) == (0, 5, 5, 5, True)

@@ -56,6 +56,35 @@ def test_viterbi_random(oracle, ref):
         assert (np.concatenate(outs) == oracle.viterbi_decode(s, fl, cr)).all()
 
 
+def _per_call_cases():
+    """(code rate, frame length, noise, depth, call size) for the per-call path: depths other
+    than the WiFi RX's 256 (the brick honours any, sora_ext_viterbi.cpp:55-56) and call
+    sizes other than 48 (whole groups of every rate: multiples of 12)."""
+    rng = np.random.default_rng(0xDE)
+    out = []
+    for i, depth in enumerate((32, 64, 100, 200, 256, 300, 512, 1000)):
+        for cr in (0, 1, 2):
+            out.append((cr, int(rng.integers(1, 700)), int(rng.integers(-1, 6)), depth,
+                        int(rng.choice([12, 24, 48, 96, 480])), 500 + 10 * i + cr))
+    return out
+
+
+def test_viterbi_depths_and_call_sizes(oracle, ref):
+    buf = np.zeros(96000, np.uint8)
+    for cr, fl, noise, depth, call, seed in _per_call_cases():
+        s = synth.viterbi_soft(cr, fl, noise, seed=seed)
+        ref.zref_viterbi_init(fl, cr, depth)
+        d = oracle.Viterbi()
+        d.init(fl, cr, depth)
+        for k in range(0, s.size, call):
+            c = np.ascontiguousarray(s[k:k + call])
+            if c.size % 12:
+                break
+            bits = ref.zref_viterbi_decode(_p(c), c.size, _p(buf), buf.size * 8)
+            got = d.decode(c)
+            assert got.size * 8 == bits and (got == buf[:bits // 8]).all(), (cr, fl, depth, call, k)
+
+
 def test_shift_right(oracle, ref):
     rng = np.random.default_rng(5)
     for n in (1, 3, 4, 5, 9):

@@ -13,6 +13,19 @@ LIBDIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(LIBDIR, "libziria_rx.so")
 
 
+def source_hash():
+    """sha256 over the kernel sources and the C-ABI header (name + content, sorted): ties a
+    PMC summary in profiles/ to the kernels it was measured on (bench.py traffic fields)."""
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".hpp", ".h", ".py")))
+    for f in files:
+        h.update(f.encode())
+        h.update(open(os.path.join(CSRC, f), "rb").read())
+    h.update(open(os.path.join(HERE, "..", "include", "ziria_rx.h"), "rb").read())
+    return h.hexdigest()[:16]
+
+
 def _stale():
     if not os.path.exists(LIB):
         return True

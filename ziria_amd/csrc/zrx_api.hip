@@ -31,9 +31,12 @@ using namespace zrx;
 
 struct zrx_ctx {
   int device = 0;
-  int crc_blocks = 1024;          // ZRX_CRCBLOCKS: k_descramble_crc grid cap (0 = one packet per wave)
+  int crc_blocks = 1024;          // k_descramble_crc grid cap (blocks of kCrcWaves packets)
+#ifdef ZRX_EXPERIMENTS
+  // A/B builds only (scripts/build_variant.sh): environment knobs that select other kernels
   int v3dbg = 0;                  // ZRX_V3DBG: k_viterbi3 timing-experiment variants (wrong output)
-  int vit_impl = 3;              // 3: k_viterbi3 (default); 2: k_viterbi2; 1: k_viterbi (A/B references)
+  int vit_impl = 3;               // ZRX_VITERBI 3: k_viterbi3; 2: k_viterbi2; 1: k_viterbi
+#endif
   hipStream_t stream = nullptr;
   bool timing = false;
   // one set of 6 events per timed zrx_rx_dev launch since zrx_enable_timing (averaged by
@@ -51,10 +54,15 @@ struct zrx_ctx {
   int64_t* dec_off = nullptr;     // p * kDecStride
   int32_t* dec_bits = nullptr;
   int32_t* order = nullptr;       // Viterbi packet order (k_vit_order)
-  bool use_order = true;          // ZRX_ORDER=0 turns the ordering off (A/B experiments)
+  bool use_order = true;          // ZRX_ORDER=0 (experiment builds) turns the ordering off
   // rx chain: k_vit_order runs on a side stream beside k_data_fft (fork/join by events)
   hipStream_t side = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
+  // The workspace is shared by every launch of this context: a launch on a different stream
+  // than the previous one first waits for the previous launch's work (ws_free).
+  hipEvent_t ws_free = nullptr;
+  hipStream_t ws_stream = nullptr;
+  bool ws_pending = false;
   // ChannelEqualization / PilotTrack trig tables (built on first use)
   uint32_t* eq_rot = nullptr;     // 65536 x (cos, -sin) complex16
   int16_t* eq_atan = nullptr;     // 256 x 256 atan2x_lut
@@ -276,7 +284,24 @@ static int ensure_eq_tables(zrx_ctx* c) {
 }
 
 static bool order_fits(const zrx_ctx* c, int npkts) {
-  return c->vit_impl == 3 && c->use_order && c->order && npkts <= c->cap_pkts && npkts <= kOrderMax;
+#ifdef ZRX_EXPERIMENTS
+  if (c->vit_impl != 3) return false;
+#endif
+  return c->use_order && c->order && npkts <= c->cap_pkts && npkts <= kOrderMax;
+}
+
+// Every launch function starts here: a launch on a different stream than the previous one
+// waits for the previous launch's work on the shared workspace to finish.
+static int ws_acquire(zrx_ctx* c) {
+  if (!c->ws_free) ZRX_CHECK(hipEventCreateWithFlags(&c->ws_free, hipEventDisableTiming));
+  if (c->ws_pending && c->ws_stream != c->stream) ZRX_CHECK(hipStreamWaitEvent(c->stream, c->ws_free, 0));
+  return ZRX_OK;
+}
+static int ws_release(zrx_ctx* c) {
+  ZRX_CHECK(hipEventRecord(c->ws_free, c->stream));
+  c->ws_stream = c->stream;
+  c->ws_pending = true;
+  return ZRX_OK;
 }
 
 // order_ready: the caller already ran k_vit_order into c->order (rx chain, side stream)
@@ -290,19 +315,24 @@ static void launch_viterbi(zrx_ctx* c, const uint8_t* soft, const int64_t* soft_
     if (!order_ready) k_vit_order<<<1, 1024, 0, c->stream>>>(params, npkts, c->order);
     order = c->order;
   }
-  if (c->vit_impl == 1)
+  const dim3 g(blocks(npkts, v3::kRows)), b(256);
+#ifdef ZRX_EXPERIMENTS
+  if (c->vit_impl == 1) {
     k_viterbi<<<blocks(npkts, 4), 256, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits, 256);
-  else if (c->vit_impl == 3) {
-    const dim3 g(blocks(npkts, v3::kRows)), b(256);
-    switch (c->v3dbg) {   // timing experiments only (ZRX_V3DBG); 0 is the product kernel
-#define ZRX_V3(D) case D: k_viterbi3<D><<<g, b, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits, order); break;
-      ZRX_V3(1) ZRX_V3(2) ZRX_V3(4) ZRX_V3(8) ZRX_V3(16) ZRX_V3(32) ZRX_V3(64) ZRX_V3(128) ZRX_V3(256) ZRX_V3(512)
-#undef ZRX_V3
-      default: k_viterbi3<0><<<g, b, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits, order);
-    }
+    return;
   }
-  else
+  if (c->vit_impl == 2) {
     k_viterbi2<<<blocks(npkts, 4), 256, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits);
+    return;
+  }
+  switch (c->v3dbg) {   // timing experiments (ZRX_V3DBG); 0 is the product kernel
+#define ZRX_V3(D) case D: k_viterbi3<D><<<g, b, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits, order); return;
+    ZRX_V3(1) ZRX_V3(2) ZRX_V3(4) ZRX_V3(8) ZRX_V3(16) ZRX_V3(32) ZRX_V3(64) ZRX_V3(128) ZRX_V3(256) ZRX_V3(512)
+#undef ZRX_V3
+    default: break;
+  }
+#endif
+  k_viterbi3<0><<<g, b, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits, order);
 }
 
 extern "C" {
@@ -318,6 +348,7 @@ int zrx_create(zrx_ctx** out, int device, void* stream) {
   zrx_ctx* c = new zrx_ctx();
   c->device = device;
   c->stream = (hipStream_t)stream;
+#ifdef ZRX_EXPERIMENTS
   if (const char* v = std::getenv("ZRX_VITERBI")) {
     const int k = std::atoi(v);
     c->vit_impl = (k >= 1 && k <= 3) ? k : 3;
@@ -325,6 +356,17 @@ int zrx_create(zrx_ctx** out, int device, void* stream) {
   if (const char* v = std::getenv("ZRX_V3DBG")) c->v3dbg = std::atoi(v);
   if (const char* v = std::getenv("ZRX_ORDER")) c->use_order = std::atoi(v) != 0;
   if (const char* v = std::getenv("ZRX_CRCBLOCKS")) c->crc_blocks = std::atoi(v);
+  std::fprintf(stderr, "ziria_rx: EXPERIMENT build (vit_impl %d, v3dbg %d, order %d, crc_blocks %d)\n", c->vit_impl,
+               c->v3dbg, (int)c->use_order, c->crc_blocks);
+#else
+  static bool warned = false;
+  for (const char* k : {"ZRX_VITERBI", "ZRX_V3DBG", "ZRX_ORDER", "ZRX_CRCBLOCKS"})
+    if (std::getenv(k) && !warned) {
+      std::fprintf(stderr, "ziria_rx: %s is an experiment-build knob (scripts/build_variant.sh); ignored by this "
+                           "product build\n", k);
+      warned = true;
+    }
+#endif
   *out = c;
   return ZRX_OK;
 }
@@ -348,6 +390,7 @@ int zrx_destroy(zrx_ctx* c) {
   }
   for (auto& set : c->evsets)
     for (auto& e : set) (void)hipEventDestroy(e);
+  if (c->ws_free) (void)hipEventDestroy(c->ws_free);
   delete c;
   return ZRX_OK;
 }
@@ -362,6 +405,12 @@ int zrx_enable_timing(zrx_ctx* c, int on) {
   if (!c) return ZRX_EINVAL;
   c->timing = on != 0;
   c->nrec = 0;
+  // event sets for the first 64 timed launches are created here, not inside the timed region
+  while (c->timing && c->evsets.size() < 64) {
+    std::array<hipEvent_t, 6> set;
+    for (auto& e : set) ZRX_CHECK(hipEventCreate(&e));
+    c->evsets.push_back(set);
+  }
   return ZRX_OK;
 }
 
@@ -417,9 +466,11 @@ int zrx_viterbi_dev(zrx_ctx* c, const int8_t* d_soft, const int64_t* d_soft_off,
                     int npkts, uint8_t* d_out, const int64_t* d_out_off, int32_t* d_out_bits) {
   if (!c || npkts < 0) return ZRX_EINVAL;
   if (npkts == 0) return ZRX_OK;
+  const int rc = ws_acquire(c);
+  if (rc) return rc;
   launch_viterbi(c, (const uint8_t*)d_soft, d_soft_off, d_params, npkts, d_out, d_out_off, d_out_bits);
   ZRX_CHECK(hipGetLastError());
-  return ZRX_OK;
+  return ws_release(c);
 }
 
 static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_sym_off, const int32_t* d_nsym,
@@ -436,6 +487,10 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
     const int rc = ensure_eq_tables(c);
     if (rc) return rc;
     T = EqTabs{c->eq_rot, c->eq_atan};
+  }
+  {
+    const int rc = ws_acquire(c);
+    if (rc) return rc;
   }
   const uint32_t* chan = (const uint32_t*)d_chan;
   hipStream_t s = c->stream;
@@ -456,7 +511,7 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
     k_signal_fft<false><<<blocks(npkts, 64), 64, 0, s>>>((const uint4*)d_sym, d_sym_off, d_nsym, npkts,
                                                            (uint4*)c->sig_soft, chan, T);
   if (ev) ZRX_CHECK(hipEventRecord(ev[1], s));
-  k_signal_vit<<<blocks(npkts, 4), 256, 0, s>>>(c->sig_soft, d_nsym, npkts, c->vparams, d_info);
+  k_signal_vit<<<blocks(npkts, 4), 256, 0, s>>>(c->sig_soft, d_nsym, npkts, c->cap_nsym, c->vparams, d_info);
   if (ev) ZRX_CHECK(hipEventRecord(ev[2], s));
   // the Viterbi packet order needs only the headers: one block on the side stream, hidden
   // behind k_data_fft (a 1-block kernel costs ~20 us in line)
@@ -486,7 +541,7 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
                      64 * kCrcWaves, 0, s>>>(c->dec, c->dec_bits, d_info, d_payload, npkts);
   if (ev) ZRX_CHECK(hipEventRecord(ev[5], s));
   ZRX_CHECK(hipGetLastError());
-  return ZRX_OK;
+  return ws_release(c);
 }
 
 int zrx_rx_dev(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_sym_off, const int32_t* d_nsym,
@@ -542,6 +597,8 @@ int zrx_rx_stream_dev(zrx_ctx* c, const struct complex16* d_samples, const int64
     ZRX_CHECK(hipMalloc(&c->fe_chan, (size_t)nc * 256 + 256));
     c->fe_cap = nc; c->fe_sym = ns;
   }
+  rc = ws_acquire(c);                                // the front-end staging is workspace too
+  if (rc) return rc;
   const uint32_t* smp = (const uint32_t*)d_samples;
   hipStream_t s = c->stream;
   fe::k_fe_detect<<<blocks(ncap, 4), 256, 0, s>>>(smp, d_cap_off, d_cap_len, ncap, downsample, 1000, c->fe_pattern, d_det);
@@ -664,13 +721,35 @@ void __ext_sora_fft_dynamic(struct complex16* out, int unused2, int16_t nFFTSize
   __ext_sora_fft(out, nFFTSize, in, unused1);
 }
 
+// The streaming decoder behind the per-call externals.  Its trellis state lives on the GPU
+// (VitStream); the host mirrors only the brick's schedule (trellis index and bits output,
+// sora_ext_viterbi.cpp:112-149), which depends on nothing but the group count.  A call whose
+// groups reach no traceback returns 0 bits in the reference, so its soft values are only
+// queued in pinned host memory; the call that reaches a traceback runs every queued group
+// and its own in one launch and copies back exactly the bytes the schedule says it emits.
+struct VitHost {
+  bool ready = false;
+  uint32_t tr = 0, ob = 0, tr_end = 0, depth = 256;
+  int cr = 0;
+  uint8_t* pend = nullptr;         // queued soft values (pinned)
+  size_t npend = 0, cap = 0;
+  uint8_t* out = nullptr;          // pinned copy-back buffer
+  size_t out_cap = 0;
+};
+static VitHost g_vh;
+
 static int vit_init_impl(int32_t frame_len, int16_t code_rate, int16_t depth) {
   std::lock_guard<std::mutex> lk(g_mu);
   zrx_ctx* c = default_ctx();
   if (!c->vstream) ZRX_OR_DIE(hipMalloc(&c->vstream, sizeof(VitStream)));
   k_vit_init<<<1, 64, 0, c->stream>>>(c->vstream, frame_len, code_rate, depth);
   ZRX_OR_DIE(hipGetLastError());
-  ZRX_OR_DIE(hipStreamSynchronize(c->stream));
+  g_vh.ready = true;
+  g_vh.tr = 0; g_vh.ob = 0;
+  g_vh.tr_end = (uint32_t)frame_len * 8u + 6u;
+  g_vh.depth = (uint32_t)depth;
+  g_vh.cr = code_rate;
+  g_vh.npend = 0;                                    // groups of the previous frame: no output left
   return 0;
 }
 
@@ -686,23 +765,49 @@ int16_t __ext_viterbi_brick_decode_fast(int8_t* intInput, int len1, unsigned cha
   if (len1 <= 0) return 0;
   std::lock_guard<std::mutex> lk(g_mu);
   zrx_ctx* c = default_ctx();
-  if (!c->vstream) ZRX_DIE("__ext_viterbi_brick_decode_fast before __ext_viterbi_brick_init_fast");
-  const size_t out_cap = (size_t)len1 + 512;
-  uint8_t* d = (uint8_t*)staging(c, (size_t)len1 + out_cap + 64);
-  if (!d) ZRX_DIE("staging allocation failed");
-  uint8_t* d_out = d + ((len1 + 15) / 16) * 16;
-  int32_t* d_bits = (int32_t*)(d_out + out_cap);
-  ZRX_OR_DIE(hipMemcpyAsync(d, intInput, (size_t)len1, hipMemcpyHostToDevice, c->stream));
-  k_viterbi_stream<<<1, 64, 0, c->stream>>>(c->vstream, d, len1, d_out, d_bits);
-  ZRX_OR_DIE(hipGetLastError());
-  int32_t bits = 0;
-  ZRX_OR_DIE(hipMemcpyAsync(&bits, d_bits, 4, hipMemcpyDeviceToHost, c->stream));
-  ZRX_OR_DIE(hipStreamSynchronize(c->stream));
-  if (bits > 0) {
-    ZRX_OR_DIE(hipMemcpyAsync(bit, d_out, (size_t)bits / 8, hipMemcpyDeviceToHost, c->stream));
-    ZRX_OR_DIE(hipStreamSynchronize(c->stream));
+  if (!c->vstream || !g_vh.ready) ZRX_DIE("__ext_viterbi_brick_decode_fast before __ext_viterbi_brick_init_fast");
+  VitHost& h = g_vh;
+  const int G = h.cr == 0 ? 2 : h.cr == 1 ? 3 : h.cr == 2 ? 4 : 0;
+  const uint32_t steps = h.cr == 0 ? 1u : h.cr == 1 ? 2u : 3u;
+  if (G == 0) return 0;
+  const size_t n = (size_t)(len1 / G) * G;          // whole groups (k_viterbi_stream drops a partial one)
+  uint32_t bytes = 0;                                // what this call emits (:112-149)
+  for (size_t k = 0; k < n; k += G) {
+    h.tr += steps;
+    uint32_t cnt = 0;
+    if (h.tr >= h.tr_end) cnt = h.tr_end - h.ob - 6u;
+    else if (h.tr >= h.ob + h.depth + 30u) cnt = h.depth;
+    if (cnt) { bytes += cnt >> 3; h.ob += cnt; }
   }
-  return (int16_t)bits;
+  if (h.npend + n > h.cap) {
+    const size_t cap = std::max<size_t>(h.npend + n, std::max<size_t>(2 * h.cap, 1 << 16));
+    uint8_t* np = nullptr;
+    ZRX_OR_DIE(hipHostMalloc((void**)&np, cap, hipHostMallocDefault));
+    if (h.npend) std::memcpy(np, h.pend, h.npend);
+    if (h.pend) (void)hipHostFree(h.pend);
+    h.pend = np; h.cap = cap;
+  }
+  std::memcpy(h.pend + h.npend, intInput, n);
+  h.npend += n;
+  if (bytes == 0) return 0;                          // no traceback in this call: stays queued
+  const size_t out_cap = (size_t)h.npend + 512;      // bytes the queued groups can emit at most
+  uint8_t* d = (uint8_t*)staging(c, h.npend + out_cap + 64);
+  if (!d) ZRX_DIE("staging allocation failed");
+  uint8_t* d_out = d + ((h.npend + 15) / 16) * 16;
+  int32_t* d_bits = (int32_t*)(d_out + out_cap);
+  if (bytes > h.out_cap) {
+    if (h.out) (void)hipHostFree(h.out);
+    h.out_cap = std::max<size_t>(bytes, 4096);
+    ZRX_OR_DIE(hipHostMalloc((void**)&h.out, h.out_cap, hipHostMallocDefault));
+  }
+  ZRX_OR_DIE(hipMemcpyAsync(d, h.pend, h.npend, hipMemcpyHostToDevice, c->stream));
+  k_viterbi_stream<<<1, 64, 0, c->stream>>>(c->vstream, d, (int)h.npend, d_out, d_bits);
+  ZRX_OR_DIE(hipGetLastError());
+  ZRX_OR_DIE(hipMemcpyAsync(h.out, d_out, bytes, hipMemcpyDeviceToHost, c->stream));
+  ZRX_OR_DIE(hipStreamSynchronize(c->stream));
+  std::memcpy(bit, h.out, bytes);
+  h.npend = 0;
+  return (int16_t)(bytes * 8u);
 }
 
 int16_t __ext_viterbiSig11a_brick_decode_fast(int8_t* intInput, int len1, unsigned char* bit, int len2) {

@@ -293,10 +293,10 @@ __device__ __forceinline__ uint32_t vit_normalize(uint32_t m) {
 // traceback (csrc/viterbicore.hpp:170-239).  Start = argmin of the SIGNED int16 key
 // (m<<8)|(4s) (SSE2 hmin16, :79-96); the state's own survivor bit rides in bit 6.
 // surv(t) returns the 64-bit survivor word of column t (bit s = LSB of m_t[s]).
-// Returns, in lane j, output byte j (bytes 0 .. nbits/8-1 in stream order).
+// Writes output bytes 0 .. nbits/8-1 (stream order) to out[] from lane 0; any depth.
 template <class SurvRead>
-__device__ __forceinline__ uint32_t vit_traceback(uint32_t m, uint32_t col, uint32_t nbits,
-                                                  uint32_t lookahead, int lane, SurvRead surv) {
+__device__ __forceinline__ void vit_traceback(uint32_t m, uint32_t col, uint32_t nbits, uint32_t lookahead,
+                                              int lane, SurvRead surv, uint8_t* __restrict__ out) {
   int key = (int)(int16_t)(uint16_t)((m << 8) | ((uint32_t)lane << 2));
   key = wave_min_i32(key);
   uint32_t i = (uint32_t)(key >> 2) & 0x7Fu;
@@ -307,7 +307,6 @@ __device__ __forceinline__ uint32_t vit_traceback(uint32_t m, uint32_t col, uint
     i |= (uint32_t)((surv(t) >> i) & 1u) << 6;
   }
   const int nbytes = (int)(nbits >> 3);
-  uint32_t mine = 0;
   for (int byte = nbytes - 1; byte >= 0; byte--) {
     uint32_t oc = 0;
 #pragma unroll
@@ -317,9 +316,8 @@ __device__ __forceinline__ uint32_t vit_traceback(uint32_t m, uint32_t col, uint
       i = (i >> 1) & 0x3Fu;
       i |= (uint32_t)((surv(t) >> i) & 1u) << 6;
     }
-    if (lane == byte) mine = oc;
+    if (lane == 0) out[byte] = (uint8_t)oc;
   }
-  return mine;
 }
 
 // ------------------------------------------------------------------ descrambler / CRC helpers

@@ -9,8 +9,8 @@
 //                    Demap{mod} -> Deinterleave{mod} (Decode.blk:45-60); with EQ, ChannelEqualization
 //                    + PilotTrack after the FFT (receiver.blk:66-71), also in k_signal_fft
 //   k_ofdm_eq        FFT -> ChannelEqualization -> PilotTrack, full 64-bin output
-//   k_viterbi        one wave per packet, lane = trellis state: the whole brick driver loop
-//                    (sora_ext_viterbi.cpp:66-153) with the survivor history in an LDS ring
+//   k_viterbi3       (zrx_viterbi3.hpp) the batched brick driver loop, four packets per wave
+//   k_viterbi        (experiment builds only) one wave per packet, lane = trellis state
 //   k_descramble_crc one wave per packet: descrambler (Decode.blk:36-43) + CRC-32 check
 //                    (crc.blk:85-118), 64 lanes each on a chunk, CRC combined by GF(2) maps
 //   k_viterbi_stream / k_vit_init / k_sig_bytes / k_shift_right: the per-call externals.
@@ -18,7 +18,9 @@
 #include <stdint.h>
 
 #include "zrx_device.hpp"
-#include "zrx_viterbi2.hpp"
+#ifdef ZRX_EXPERIMENTS
+#include "zrx_viterbi2.hpp"   // k_viterbi2: A/B builds only (scripts/build_variant.sh)
+#endif
 #include "zrx_viterbi3.hpp"
 #include "zrx_frontend.hpp"
 #include "zrx_tx.hpp"
@@ -162,8 +164,10 @@ __device__ __forceinline__ int ndbps_of(int mod, int coding) {
 // SIGNAL Viterbi + parsePLCPHeader -> Viterbi/FFT parameters and packet info.
 // vparams[4p..] = {frame_len, code_rate, soft_len, modulation}
 // info[8p..]    = {modulation, coding, len, header_err, crc_ok, status, symbols_used, viterbi_bits}
+// cap_nsym: symbols per packet the soft workspace holds (zrx_reserve); a packet whose header
+// asks for more gets ZRX_PKT_OVERSIZE and no soft values, so nothing writes past its slot.
 __global__ __launch_bounds__(256) void k_signal_vit(const uint32_t* __restrict__ sig_soft, const int32_t* __restrict__ nsym,
-                                                    int npkts, int32_t* __restrict__ vparams,
+                                                    int npkts, int cap_nsym, int32_t* __restrict__ vparams,
                                                     int32_t* __restrict__ info) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int p = blockIdx.x * 4 + wv;
@@ -192,6 +196,7 @@ __global__ __launch_bounds__(256) void k_signal_vit(const uint32_t* __restrict__
   int status = 0;
   if (err) status = 1;
   else if (need > nsym[p] - 1) status = 2;
+  else if (need > cap_nsym - 1) status = 3;
   if (lane == 0) {
     int32_t* vp = vparams + 4 * (int64_t)p;
     vp[0] = len + 2;                                  // Decode.blk:59 Viterbi(h.coding, h.len+2)
@@ -298,14 +303,14 @@ __device__ __forceinline__ void vit_after_group(VitRun& v, int lane, Surv surv, 
     look = 24u + (v.tr - (v.ob + v.depth + 30u)) % 8u;
   }
   if (cnt) {
-    const uint32_t byte = vit_traceback(v.m, v.tr, cnt, look, lane, surv);
+    vit_traceback(v.m, v.tr, cnt, look, lane, surv, out + v.total_bytes);
     const uint32_t nb = cnt >> 3;
-    if ((uint32_t)lane < nb) out[v.total_bytes + lane] = (uint8_t)byte;
     v.ob += cnt;
     v.total_bytes += nb;
   }
 }
 
+#ifdef ZRX_EXPERIMENTS   // the v1 batched kernel (lane = state): A/B builds only
 template <int USE>
 __device__ __forceinline__ void vit_step(VitRun& v, int a, int b, const VitLane& L, int lane, uint64_t* ring) {
   v.m = acs<USE>(v.m, a, b, L);
@@ -372,6 +377,8 @@ __global__ __launch_bounds__(256) void k_viterbi(const uint8_t* __restrict__ sof
   }
   if (lane == 0) out_bits[p] = (int32_t)(v.total_bytes * 8u);
 }
+
+#endif  // ZRX_EXPERIMENTS
 
 // ------------------------------------------------------------------ descramble + CRC
 // info[8p+4] = crc_ok, info[8p+7] = viterbi bits; payload gets len-4 descrambled bytes.

@@ -1,15 +1,29 @@
-"""Packet sharding across the GPUs of one node.
+"""Packet sharding across the GPUs of one node (BASELINE config 4).
 
 Packets are independent, so a batch is split into contiguous packet ranges, one per rank,
 and decoded with no collective in the hot loop.  After decoding, one exchange over
 torch.distributed (RCCL over xGMI on the GPU node; gloo in the CPU tests) combines the
 per-rank results: a sum of {CRC-pass count, payload bits, bit-exact flags} and a gather of
-the decoded payload bytes to the destination rank.  The reference has no distributed code
-(its only parallelism is intra-process pipeline threading, src/Pipeline/PassPipeline.hs:144),
-so this is new, and it never changes per-packet results.
+the decoded payload bytes and packet infos to the destination rank, where every packet is
+checked against what was transmitted.  The reference has no distributed code (its only
+parallelism is intra-process pipeline threading, src/Pipeline/PassPipeline.hs:144), so this
+is new, and it never changes per-packet results.
+
+`run_sharded` is the whole N-rank bench step loop (bench.py drives it with the HIP engine,
+tests/test_node.py with a stub decoder over gloo), so the path the driver's 1/2/4/8-GPU
+runs take is the path the CPU tests cover.
 """
+import time
+
+import numpy as np
 import torch
 import torch.distributed as dist
+
+
+def world_rank():
+    if dist.is_initialized():
+        return dist.get_world_size(), dist.get_rank()
+    return 1, 0
 
 
 def shard_range(npkts, world, rank):
@@ -36,28 +50,114 @@ def counts(info, payload_len=None, payload=None, expected=None, crc_ok_only=Fals
     return ok, bits, match
 
 
+def gather_rows(t, dst=0):
+    """Gathers a [n_r, ...] tensor from every rank to `dst`, where n_r may differ per rank
+    (unequal shards): each rank pads to the largest n_r, the padded blocks are gathered,
+    and `dst` trims them.  Returns the row-wise concatenation in rank order on `dst`
+    (the tensor itself with one rank), None elsewhere."""
+    world, rank = world_rank()
+    if world == 1:
+        return t
+    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    sizes = [int(s.item()) for s in sizes]
+    cap = max(sizes)
+    pad = torch.zeros((cap,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    pad[:t.shape[0]] = t
+    blocks = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
+    dist.gather(pad, blocks, dst=dst)
+    if rank != dst:
+        return None
+    return torch.cat([b[:s] for b, s in zip(blocks, sizes)], 0)
+
+
 def combine(ok, bits, match, payload=None, dst=0, device=None):
     """Sums the per-rank counts over the default process group and gathers `payload`
-    ([n, L] uint8, the same shape on every rank) to `dst`.  Returns
-    (ok_total, bits_total, ranks_matching, gathered list or None)."""
-    world = dist.get_world_size() if dist.is_initialized() else 1
-    t = torch.tensor([ok, bits, match], dtype=torch.int64, device=device)
+    ([n_r, L] uint8; n_r may differ per rank) to `dst`.  Returns (ok_total, bits_total,
+    ranks_matching, gathered payload rows on dst or None)."""
+    world, _ = world_rank()
     if world == 1:
-        return ok, bits, match, ([payload] if payload is not None else None)
+        return ok, bits, match, payload
+    t = torch.tensor([ok, bits, match], dtype=torch.int64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    gathered = None
-    if payload is not None:
-        rank = dist.get_rank()
-        gathered = [torch.empty_like(payload) for _ in range(world)] if rank == dst else None
-        dist.gather(payload, gathered, dst=dst)
+    gathered = gather_rows(payload, dst) if payload is not None else None
     o, b, m = (int(v) for v in t.tolist())
     return o, b, m, gathered
 
 
 def max_over_ranks(seconds, device=None):
     """The slowest rank's elapsed time (the bench's timing rule)."""
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    world, _ = world_rank()
+    if world == 1:
         return seconds
     t = torch.tensor([seconds], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def barrier(device=None):
+    if world_rank()[0] > 1:
+        dist.barrier()
+
+
+def _sync(device):
+    if device is not None and device.type == "cuda":
+        torch.cuda.synchronize(device)
+
+
+def run_sharded(total, make_shard, step, outputs, expected, steps, warmup, payload_len, device=None,
+                crc_ok_only=False, on_timed=None):
+    """The bench's N-rank loop over one global batch of `total` packets.
+
+    make_shard(lo, hi) builds this rank's packets [lo, hi) (already in device memory);
+    step(shard) runs one decode of the shard; outputs(shard) -> (payload uint8 [n, >=L],
+    info int32 [n, 8]) of the last step; expected(lo, hi) -> uint8 numpy [hi-lo, L], the
+    transmitted payloads (L = payload_len bytes each), which rank 0 uses to check every
+    gathered packet.
+    on_timed(True/False) is called right before / after the timed steps (stage timers).
+
+    Timing: `warmup` untimed steps, then barrier + device sync, `steps` timed steps, device
+    sync + barrier, and the slowest rank's time.  Returns on every rank a dict with the
+    shard, the timing and the combined counts; rank 0's also holds the per-packet check."""
+    world, rank = world_rank()
+    lo, hi = shard_range(total, world, rank)
+    shard = make_shard(lo, hi)
+    for _ in range(warmup):
+        step(shard)
+    _sync(device)
+    barrier(device)
+    _sync(device)
+    if on_timed:
+        on_timed(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(shard)
+    _sync(device)
+    barrier(device)
+    t1 = time.perf_counter()
+    if on_timed:
+        on_timed(False)
+    elapsed = max_over_ranks(t1 - t0, device=device)
+
+    payload, info = outputs(shard)
+    L = payload_len
+    ok, bits, _ = counts(info)
+    _sync(device)
+    tg = time.perf_counter()
+    ok_all, bits_all, _, pay_all = combine(ok, bits, 1, payload[:, :L].contiguous(), device=device)
+    info_all = gather_rows(info.contiguous())
+    _sync(device)
+    gather_s = time.perf_counter() - tg
+    res = dict(lo=lo, hi=hi, shard=shard, elapsed=elapsed, steps=steps, ok=ok_all, bits=bits_all,
+               gather_s=gather_s, world=world, rank=rank)
+    if rank == 0:
+        pay = pay_all.cpu().numpy()
+        inf = info_all.cpu().numpy()
+        exp = np.asarray(expected(0, total))
+        crc = inf[:, 4] == 1
+        same = (pay[:, :exp.shape[1]] == exp).all(axis=1)
+        res["packets"] = int(pay.shape[0])
+        res["payload_match"] = bool(same[crc].all() if crc_ok_only else same.all())
+        res["mismatched_packets"] = int((~same & (crc if crc_ok_only else True)).sum())
+    return res

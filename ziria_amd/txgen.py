@@ -5,7 +5,7 @@ This is a workload generator, not part of the decode path.  It restates the tran
 (code/WiFi/transmitter/transmitter.blk:56-101: crc + SERVICE + pad, scrambler 1011101,
 encode12/23/34, interleave, modulate) and the channel of SURVEY.md Appendix E:
 x = IDFT(X / 100) * 64 + N(0, sigma^2) per component, rounded to int16.
-tests/test_txgen.py checks it against the oracle's transmitter restatement.
+tests/test_tables_txgen.py checks it against the oracle's transmitter restatement.
 """
 import zlib
 
@@ -240,3 +240,51 @@ def make_mixed(n, min_len=64, max_len=4095, sigma=4.0, seed=0x3C5, device="cpu",
     return dict(sym=torch.cat(syms, 0), sym_off=torch.tensor(offs, dtype=torch.int64, device=device),
                 nsym=torch.tensor(nsyms, dtype=torch.int32, device=device), payload=pays,
                 meta=np.array(meta, np.int32), max_nsym=int(max(nsyms)))
+
+
+def _chunk_seeds(seed, c):
+    return np.random.default_rng([seed, c]), (seed * 1000003 + 7919 * c) & 0x7FFFFFFFFFFF
+
+
+def payloads_range(lo, hi, payload_len=1500, seed=0x5EED, chunk=2048):
+    """Payloads of global packets [lo, hi) of make_batch_range (numpy uint8 [hi-lo, L])."""
+    out = []
+    for c in range(lo // chunk, (hi + chunk - 1) // chunk):
+        rng, _ = _chunk_seeds(seed, c)
+        p = rng.integers(0, 256, (chunk, payload_len), dtype=np.uint8)
+        a, b = max(lo, c * chunk) - c * chunk, min(hi, (c + 1) * chunk) - c * chunk
+        out.append(p[a:b])
+    return np.concatenate(out, 0) if out else np.zeros((0, payload_len), np.uint8)
+
+
+def make_batch_range(lo, hi, mod=3, coding=2, payload_len=1500, sigma=4.0, seed=0x5EED, device="cpu", chunk=2048,
+                     channel=False):
+    """Global packets [lo, hi) of a batch whose packet i depends only on (seed, i): chunk c
+    of `chunk` packets draws its payloads and noise from generators seeded by (seed, c), so
+    a rank that builds its contiguous shard gets exactly the packets a single GPU decoding
+    the whole batch would (BASELINE config 4: same per-packet outputs).  Same dict as
+    make_batch, for the hi-lo packets of the range."""
+    S = 1 + n_data_symbols(mod, coding, payload_len)
+    syms, chans, pays = [], [], []
+    for c in range(lo // chunk, (hi + chunk - 1) // chunk):
+        rng, tseed = _chunk_seeds(seed, c)
+        p = rng.integers(0, 256, (chunk, payload_len), dtype=np.uint8)
+        a, b = max(lo, c * chunk) - c * chunk, min(hi, (c + 1) * chunk) - c * chunk
+        gen = torch.Generator(device=device)
+        gen.manual_seed(tseed)
+        f = packets_freq(p, mod, coding, device)
+        t = to_time(f, sigma, gen, channel=channel)
+        if channel:
+            t, ch = t
+            chans.append(ch[a:b])
+        syms.append(t[a:b].reshape(-1, 64, 2))
+        pays.append(p[a:b])
+    n = hi - lo
+    d = dict(sym=torch.cat(syms, 0) if syms else torch.zeros((0, 64, 2), dtype=torch.int16, device=device),
+             sym_off=torch.arange(n, dtype=torch.int64, device=device) * S,
+             nsym=torch.full((n,), S, dtype=torch.int32, device=device),
+             payload=np.concatenate(pays, 0) if pays else np.zeros((0, payload_len), np.uint8),
+             max_nsym=S, mod=mod, coding=coding, payload_len=payload_len)
+    if channel:
+        d["chan"] = torch.cat(chans, 0).contiguous()
+    return d
