@@ -61,6 +61,7 @@ __device__ __forceinline__ uint32_t pos_of(uint32_t l, uint32_t d, uint32_t h) {
 // Per-lane constants (registers for the whole kernel).
 struct Consts {
   uint32_t sel[6][2];     // v_perm selector: [BM_hi][bm_hi<<7][BM_lo][bm_lo<<7]
+  uint32_t sel7[3][2];    // KPH 7 columns (phases 1, 3, 5): [BM_hi + bm_hi][0][BM_lo + bm_lo][0]
   uint32_t cf[6][2];      // per half (28 + bm) << 8: BY = cf - BX for a full column
   uint32_t cs[6][2];      // per half (14 + bm) << 8: punctured column
   uint32_t sa[3][4];      // LDS ring byte offset of the state held by position q at C mod 6 = 0,2,4
@@ -71,7 +72,7 @@ __device__ __forceinline__ void make_consts(Consts& K, uint32_t l, uint32_t rib)
   for (int ph = 0; ph < 6; ph++) {
 #pragma unroll
     for (int d = 0; d < 2; d++) {
-      uint32_t s = 0, cf = 0, cs = 0;
+      uint32_t s = 0, s7 = 0, cf = 0, cs = 0;
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         const uint32_t j = rotl6(pos_of(l, d, h), ph);
@@ -80,10 +81,14 @@ __device__ __forceinline__ void make_consts(Consts& K, uint32_t l, uint32_t rib)
         const uint32_t B = (j ^ (j >> 1) ^ (j >> 2)) & 1u;          // (encoding.blk:92-109)
         s |= (bm ? 4u : 12u) << (16 * h);
         s |= (2u * A + B) << (16 * h + 8);
+        // KPH 7: byte 2A+B of P (src1) or of P | 0x01010101 (src0: BM + 1, BM even), low byte 0
+        s7 |= 12u << (16 * h);
+        s7 |= (2u * A + B + (bm ? 4u : 0u)) << (16 * h + 8);
         cf |= (28u + bm) << (16 * h + 8);
         cs |= (14u + bm) << (16 * h + 8);
       }
       K.sel[ph][d] = s; K.cf[ph][d] = cf; K.cs[ph][d] = cs;
+      if (ph & 1) K.sel7[ph >> 1][d] = s7;
     }
   }
 #pragma unroll
@@ -195,15 +200,11 @@ __device__ __forceinline__ void column5(uint32_t& M0, uint32_t& M1, uint32_t P, 
   // tests/test_vit3_model.py checks both selector identities.
   constexpr uint32_t mbits = KPH == 7 ? 0x01000100u : mk * 0x00010001u;
   uint32_t BX0, BX1;
-  if constexpr (KPH == 7) {
-    BX0 = __builtin_amdgcn_perm(0x80808080u, P, K.sel[PH][0]);
-    BX0 += BX0 & 0x00FF00FFu;
-    if constexpr (PH == 2) BX1 = BX0;
-    else if constexpr (PH == 4) BX1 = BX0 ^ mbits;
-    else {
-      BX1 = __builtin_amdgcn_perm(0x80808080u, P, K.sel[PH][1]);
-      BX1 += BX1 & 0x00FF00FFu;
-    }
+  if constexpr (KPH == 7) {        // [BM + bm][0] per half: BM (even) or BM + 1 = byte of P | 0x01010101
+    static_assert(PH & 1, "KPH 7 columns have odd phases (body columns 5, 13, 21)");
+    const uint32_t P1 = P | 0x01010101u;
+    BX0 = __builtin_amdgcn_perm(P1, P, K.sel7[PH >> 1][0]);
+    BX1 = __builtin_amdgcn_perm(P1, P, K.sel7[PH >> 1][1]);
   } else {
     BX0 = __builtin_amdgcn_perm((mk & 0xFFu) * 0x01010101u, P, K.sel[PH][0]);
     if constexpr (PH == 2) BX1 = BX0;
@@ -220,9 +221,9 @@ __device__ __forceinline__ void column5(uint32_t& M0, uint32_t& M1, uint32_t P, 
   } else if constexpr (PH == 4) {
     Z0 = T1 + BY0;
     Z1 = T0 + BY1;
-  } else {
-    Z0 = w32(h2(T0).yx + h2(BY0));
-    Z1 = w32(h2(T1).yx + h2(BY1));
+  } else {                         // partner = the other half: [T.lo + BY.hi][T.hi + BY.lo] in one op
+    asm("v_pk_add_u16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(Z0) : "v"(T0), "v"(BY0));
+    asm("v_pk_add_u16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(Z1) : "v"(T1), "v"(BY1));
   }
   M0 = w32(__builtin_elementwise_min(h2(X0), h2(Z0)));
   M1 = w32(__builtin_elementwise_min(h2(X1), h2(Z1)));
@@ -506,34 +507,33 @@ __global__ __launch_bounds__(256, 4) void k_viterbi3(const uint8_t* __restrict__
     fl = vp[0]; cr = vp[1]; n = vp[2];
     so = soft_off[p]; oo = out_off[p];
   }
-  v3::Row R;
-  R.ob = 0; R.end = (uint32_t)fl * 8u + 6u;
-  R.cols = valid && n > 0 && cr >= 0 && cr <= 2 ? (uint32_t)(n / (cr == 0 ? 2 : cr == 1 ? 3 : 4)) * (uint32_t)(cr + 1) : 0u;
-  R.live = R.cols > 0;
-  R.ppend = R.fpend = false;
-  R.pT = R.plook = R.fT = R.fcnt = R.flook = 0;
-  R.pM0 = R.pM1 = R.fM0 = R.fM1 = 0;
-  R.nbytes = 0;
-  R.next = v3::row_next(R);
+  const uint32_t cols = valid && n > 0 && cr >= 0 && cr <= 2 ? (uint32_t)(n / (cr == 0 ? 2 : cr == 1 ? 3 : 4)) * (uint32_t)(cr + 1) : 0u;
   v3::Consts K;
   v3::make_consts(K, l, rib);
   const uint8_t* sp = soft + so;
   // output bytes are addressed as out + 32-bit offset (one uniform base for the whole wave)
   uint8_t* obase = out + (oo & ~(int64_t)0xFFFFFFFF);
   const uint32_t ooff = (uint32_t)(oo & 0xFFFFFFFF);
-  // rows of one rate run together; other rows of the wave sit out that pass
+  uint32_t nbytes = 0;
+  // rows of one rate run together; other rows of the wave sit out that pass.  The row state
+  // is built per pass (not kept across passes), which keeps it out of the register budget.
   for (int rate = 0; rate < 3; rate++) {
-    const bool mine = R.live && cr == rate;
+    const bool mine = cols > 0 && cr == rate;
     if (__builtin_amdgcn_ballot_w64(mine) == 0) continue;
-    v3::Row Rr = R;
+    v3::Row Rr;
+    Rr.ob = 0; Rr.end = (uint32_t)fl * 8u + 6u; Rr.cols = cols;
     Rr.live = mine;
+    Rr.ppend = Rr.fpend = false;
+    Rr.pT = Rr.plook = Rr.fT = Rr.fcnt = Rr.flook = 0;
+    Rr.pM0 = Rr.pM1 = Rr.fM0 = Rr.fM1 = 0;
+    Rr.nbytes = 0;
     Rr.next = v3::row_next(Rr);
     if (rate == 0) v3::run_rows<0, DBG>(sp, (uint32_t)max(n, 0), Rr, K, l, rib, ring, obase, ooff);
     else if (rate == 1) v3::run_rows<1, DBG>(sp, (uint32_t)max(n, 0), Rr, K, l, rib, ring, obase, ooff);
     else v3::run_rows<2, DBG>(sp, (uint32_t)max(n, 0), Rr, K, l, rib, ring, obase, ooff);
-    if (mine) R.nbytes = Rr.nbytes;
+    if (mine) nbytes = Rr.nbytes;
   }
-  if (valid && l == 0) out_bits[p] = (int32_t)(R.nbytes * 8u);
+  if (valid && l == 0) out_bits[p] = (int32_t)(nbytes * 8u);
 }
 
 // Packet order for k_viterbi3 over a mixed batch (BASELINE config 5): by code rate, then by
