@@ -58,6 +58,11 @@ __device__ __forceinline__ uint32_t pos_of(uint32_t l, uint32_t d, uint32_t h) {
   return h | (d << 1) | (b2 << 2) | (b3 << 3) | (b4 << 4) | (b5 << 5);
 }
 
+// LDS byte address of a pointer into a __shared__ array (for inline-asm DS instructions)
+__device__ __forceinline__ uint32_t lds_addr(const uint8_t* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)p;
+}
+
 // Per-lane constants (registers for the whole kernel).
 struct Consts {
   uint32_t sel[6][2];     // v_perm selector: [BM_hi][bm_hi<<7][BM_lo][bm_lo<<7]
@@ -341,12 +346,25 @@ __device__ __forceinline__ void traceback(bool due, uint32_t M0, uint32_t M1, ui
   nbytes = max(nbytes, ((c_hi - 14u) >> 3) + 1u);
 }
 
-// P word of one column from its soft values (a, b) (BM(v, e) = e ? 14-2v : 2v, viterbilut.h)
-__device__ __forceinline__ uint32_t p_word(uint32_t r, uint32_t a, uint32_t b) {
-  // 2v replicated into 4 bytes with v_perm (v_mul_lo_u32 is a quarter-rate instruction)
-  const uint32_t a2 = __builtin_amdgcn_perm(0u, (a & 7u) << 1, 0u), b2 = __builtin_amdgcn_perm(0u, (b & 7u) << 1, 0u);
-  const uint32_t pa = a2 ^ 0x0E0E0000u, pb = a2 ^ 0x0E000E00u;
-  return r == 0 ? pa + (b2 ^ 0x0E000E00u) : (r == 1 ? pa : pb);
+// P word of one column from its soft values (a, b) (BM(v, e) = e ? 14-2v : 2v, viterbilut.h):
+// [BM(0,0), BM(0,1), BM(1,0), BM(1,1)] = (2a replicated ^ X) + ((2b replicated & Mb) ^ Y),
+// with the lane's column kind in per-lane constants instead of selects (v_cndmask costs ~20
+// cycles per wave on gfx950, profiles/r01_ubench_isa_costs.log):
+//   full column (a on A, b on B): X = 0x0E0E0000, Mb = ~0, Y = 0x0E000E00
+//   A only:                        X = 0x0E0E0000, Mb = 0,  Y = 0
+//   B only (a on B):               X = 0x0E000E00, Mb = 0,  Y = 0
+struct PKind {
+  uint32_t X, Mb, Y;
+};
+__device__ __forceinline__ PKind p_kind(uint32_t r) {
+  return r == 0 ? PKind{0x0E0E0000u, 0xFFFFFFFFu, 0x0E000E00u}
+                : (r == 1 ? PKind{0x0E0E0000u, 0u, 0u} : PKind{0x0E000E00u, 0u, 0u});
+}
+__device__ __forceinline__ uint32_t p_word(const PKind& k, uint32_t a, uint32_t b) {
+  // v replicated into 4 bytes (v_perm), doubled and masked to 2(v & 7) in each byte
+  const uint32_t a2 = (__builtin_amdgcn_perm(0u, a, 0u) << 1) & 0x0E0E0E0Eu;
+  const uint32_t b2 = (__builtin_amdgcn_perm(0u, b, 0u) << 1) & (0x0E0E0E0Eu & k.Mb);
+  return (a2 ^ k.X) + (b2 ^ k.Y);
 }
 
 // DBG (timing experiments only, never selected by default): 1 skip the traceback walk,
@@ -395,10 +413,16 @@ struct Packet {
     if constexpr (c % 8 == 6 && !(DBG & 2)) {          // snapshot column (C = 6 mod 8)
       uint8_t* s = ring + (c >> 3) * kSlotBytes;
       constexpr int sh = V5 ? 1 : 0;                   // v5: the decisions are bits 8..1
-      s[K.sa[c >> 3][0]] = (uint8_t)(M0 >> sh);
-      s[K.sa[c >> 3][1]] = (uint8_t)(M0 >> (16 + sh));
-      s[K.sa[c >> 3][2]] = (uint8_t)(M1 >> sh);
-      s[K.sa[c >> 3][3]] = (uint8_t)(M1 >> (16 + sh));
+      // one shift per dword: byte 0 by ds_write_b8, byte 2 by ds_write_b8_d16_hi (asm: the
+      // compiler folds (x >> 1) >> 16 back into a second shift)
+      const uint32_t u0 = M0 >> sh, u1 = M1 >> sh;
+      s[K.sa[c >> 3][0]] = (uint8_t)u0;
+      s[K.sa[c >> 3][2]] = (uint8_t)u1;
+      const uint32_t b0 = lds_addr(ring);
+      asm volatile("ds_write_b8_d16_hi %0, %1 offset:%2" ::"v"(b0 + K.sa[c >> 3][1]), "v"(u0),
+                   "i"((c >> 3) * kSlotBytes) : "memory");
+      asm volatile("ds_write_b8_d16_hi %0, %1 offset:%2" ::"v"(b0 + K.sa[c >> 3][3]), "v"(u1),
+                   "i"((c >> 3) * kSlotBytes) : "memory");
     }
     if constexpr (c % RT::steps == 0) {                // group end
       if constexpr (c % 8 == 0 && (CR != 2 || c == 24) && !(DBG & 4)) normalize(M0, M1);
@@ -449,15 +473,16 @@ __device__ void run_rows(const uint8_t* __restrict__ sp, uint32_t n, Row& R, con
   auto fetch = [&](uint32_t base, uint32_t o, uint32_t r, uint32_t& a, uint32_t& b) {
     const uint32_t i = min(base + o, last);
     a = sp[i];
-    b = r == 0 ? sp[min(i + 1u, last)] : 0u;
+    b = sp[min(i + 1u, last)];                         // used by full columns only (PKind.Mb)
   };
+  const PKind k1 = p_kind(r1), k2 = p_kind(r2);
   uint32_t a1, b1, a2, b2;
   fetch(0, o1, r1, a1, b1);
   fetch(0, o2, r2, a2, b2);
   uint32_t s_next = wave_min_rows(R.next);
   uint32_t slot = 0;                                   // first slot of this body (3 per body)
   for (uint32_t tr0 = 0, base = 0; __builtin_amdgcn_ballot_w64(R.live) != 0; tr0 += 24, base += RT::chunk) {
-    const uint32_t Pa = p_word(r1, a1, b1), Pb = p_word(r2, a2, b2);
+    const uint32_t Pa = p_word(k1, a1, b1), Pb = p_word(k2, a2, b2);
     fetch(base + RT::chunk, o1, r1, a1, b1);           // next body's soft values (latency hidden)
     fetch(base + RT::chunk, o2, r2, a2, b2);
     pk.ring = ring_block + slot * kSlotBytes;
