@@ -70,6 +70,7 @@ struct Consts {
   uint32_t cf[6][2];      // per half (28 + bm) << 8: BY = cf - BX for a full column
   uint32_t cs[6][2];      // per half (14 + bm) << 8: punctured column
   uint32_t sa[3][4];      // LDS ring byte offset of the state held by position q at C mod 6 = 0,2,4
+  uint32_t sa2w;          // C mod 6 = 4: the 4 states of the lane are the ring dword at this offset
 };
 
 __device__ __forceinline__ void make_consts(Consts& K, uint32_t l, uint32_t rib) {
@@ -100,6 +101,7 @@ __device__ __forceinline__ void make_consts(Consts& K, uint32_t l, uint32_t rib)
   for (int k = 0; k < 3; k++)
 #pragma unroll
     for (int q = 0; q < 4; q++) K.sa[k][q] = rib * 64u + rev6(rotl6(pos_of(l, q >> 1, q & 1), 2 * k));
+  K.sa2w = K.sa[2][0] & ~3u;   // k = 2: dword address of the lane's 4 consecutive bytes (column5)
 }
 
 // One trellis column (phase PH = column index mod 6 before the step), KIND 0: (a, b) on
@@ -320,28 +322,57 @@ __device__ __forceinline__ void traceback(bool due, uint32_t M0, uint32_t M1, ui
   best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x4E, 0xF, 0xF, false));
   best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x141, 0xF, 0xF, false));
   best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x140, 0xF, 0xF, false));
-  if (!due || l != 0 || cnt == 0) return;
+  const bool walker = due && l == 0 && cnt != 0;
+  const uint64_t wm = __builtin_amdgcn_ballot_w64(walker);
+  if (wm == 0) return;
   const uint32_t s0 = (best >> 18) & 63u, pad = best & 0xFFu;
   // bit i of Z = decision of column T + 6 - i along the best path (state bits, then the pad)
   const uint32_t Z = s0 | ((__builtin_bitreverse32(pad) >> 24) << 6);
   const uint32_t C0 = T - ((T - 6u) & 7u);             // newest snapshot column <= T
-  uint32_t ix = __builtin_bitreverse32((Z >> (T - C0)) & 63u) >> 26;   // ring index = rev6(state)
   const uint32_t c_hi = T - look;
   const uint32_t nlook = (C0 - c_hi) >> 3, nout = cnt >> 3;
   constexpr uint32_t span = (uint32_t)kRing * kSlotBytes;
-  // previous slot: x - 1024, wrapping below slot 0 by one unsigned min (no compare + select)
-  auto prev = [](uint32_t x) { const uint32_t y = x - (uint32_t)kSlotBytes; return min(y, y + span); };
-  uint32_t a = rib * 64u + (((C0 - 6u) >> 3) % (uint32_t)kRing) * kSlotBytes;
-  for (uint32_t i = 0; i < nlook; i++) {               // lookahead blocks: state only
-    ix = ring[a + ix] & 63u;
-    a = prev(a);
-  }
+  // Do the walking rows share their window (C0, c_hi, nout)?  Then the slot sequence is
+  // wave-uniform: the slot base steps back on the scalar unit and a walk step is one
+  // v_and_or (next ring index) plus the LDS address add.  (Always the case for a batch of
+  // equal packets; mixed rows take the per-row walk below.)
+  const int first = (int)__builtin_ctzll(wm);
+  const uint32_t C0f = (uint32_t)__builtin_amdgcn_readlane((int)C0, first);
+  const uint32_t chf = (uint32_t)__builtin_amdgcn_readlane((int)c_hi, first);
+  const uint32_t nof = (uint32_t)__builtin_amdgcn_readlane((int)nout, first);
+  const bool uni = __builtin_amdgcn_ballot_w64(walker && (C0 != C0f || c_hi != chf || nout != nof)) == 0;
+  if (!walker) return;
+  const uint32_t rb = rib * 64u;
+  uint32_t ix = rb + (__builtin_bitreverse32((Z >> (T - C0)) & 63u) >> 26);   // ring index = rev6(state)
   uint8_t* op = out + ooff + ((c_hi - 14u) >> 3);      // output byte of block c_hi, newest first
-  for (uint32_t i = 0; i < nout; i++) {
-    const uint32_t b = ring[a + ix];
-    *op-- = (uint8_t)b;
-    ix = b & 63u;
-    a = prev(a);
+  if (uni) {
+    uint32_t A = (((C0f - 6u) >> 3) % (uint32_t)kRing) * kSlotBytes;   // uniform slot base
+    auto prevS = [](uint32_t x) { return x == 0u ? span - (uint32_t)kSlotBytes : x - (uint32_t)kSlotBytes; };
+    const uint32_t nl = (C0f - chf) >> 3;
+    for (uint32_t i = 0; i < nl; i++) {                // lookahead blocks: state only
+      ix = (ring[A + ix] & 63u) | rb;
+      A = prevS(A);
+    }
+    for (uint32_t i = 0; i < nout; i++) {
+      const uint32_t b = ring[A + ix];
+      *op-- = (uint8_t)b;
+      ix = (b & 63u) | rb;
+      A = prevS(A);
+    }
+  } else {
+    // previous slot: x - 1024, wrapping below slot 0 by one unsigned min (no compare + select)
+    auto prev = [](uint32_t x) { const uint32_t y = x - (uint32_t)kSlotBytes; return min(y, y + span); };
+    uint32_t a = (((C0 - 6u) >> 3) % (uint32_t)kRing) * kSlotBytes;
+    for (uint32_t i = 0; i < nlook; i++) {
+      ix = (ring[a + ix] & 63u) | rb;
+      a = prev(a);
+    }
+    for (uint32_t i = 0; i < nout; i++) {
+      const uint32_t b = ring[a + ix];
+      *op-- = (uint8_t)b;
+      ix = (b & 63u) | rb;
+      a = prev(a);
+    }
   }
   nbytes = max(nbytes, ((c_hi - 14u) >> 3) + 1u);
 }
@@ -413,9 +444,14 @@ struct Packet {
     if constexpr (c % 8 == 6 && !(DBG & 2)) {          // snapshot column (C = 6 mod 8)
       uint8_t* s = ring + (c >> 3) * kSlotBytes;
       constexpr int sh = V5 ? 1 : 0;                   // v5: the decisions are bits 8..1
+      const uint32_t u0 = M0 >> sh, u1 = M1 >> sh;
+      if constexpr (V5 && (c >> 3) == 2) {
+        // C mod 6 = 4: the lane's 4 states are 4 consecutive ring bytes, byte (h << 1) | d
+        // (rev6(rotl6(p, 4)) sends position bits 0, 1 to ring-index bits 1, 0): one dword store
+        *(uint32_t*)(s + K.sa2w) = __builtin_amdgcn_perm(u1, u0, 0x06020400u);
+      } else {
       // one shift per dword: byte 0 by ds_write_b8, byte 2 by ds_write_b8_d16_hi (asm: the
       // compiler folds (x >> 1) >> 16 back into a second shift)
-      const uint32_t u0 = M0 >> sh, u1 = M1 >> sh;
       s[K.sa[c >> 3][0]] = (uint8_t)u0;
       s[K.sa[c >> 3][2]] = (uint8_t)u1;
       const uint32_t b0 = lds_addr(ring);
@@ -423,6 +459,7 @@ struct Packet {
                    "i"((c >> 3) * kSlotBytes) : "memory");
       asm volatile("ds_write_b8_d16_hi %0, %1 offset:%2" ::"v"(b0 + K.sa[c >> 3][3]), "v"(u1),
                    "i"((c >> 3) * kSlotBytes) : "memory");
+      }
     }
     if constexpr (c % RT::steps == 0) {                // group end
       if constexpr (c % 8 == 0 && (CR != 2 || c == 24) && !(DBG & 4)) normalize(M0, M1);
