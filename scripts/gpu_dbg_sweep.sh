@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 for d in ${DBGS:-0 1 2 8 16 0}; do
-  ZRX_V3DBG=$d timeout -k 10 120 python bench.py --steps 10 --warmup 3 --no-cpu > gpurun_out/dbg_$d.log 2>&1 || exit 1
+  ZRX_LIB_VARIANT=${LIBV:-} ZRX_V3DBG=$d timeout -k 10 120 python bench.py --steps 10 --warmup 3 --no-cpu > gpurun_out/dbg_$d.log 2>&1 || exit 1
   python - "$d" <<'PY'
 import json, sys
 for l in open(f"gpurun_out/dbg_{sys.argv[1]}.log"):

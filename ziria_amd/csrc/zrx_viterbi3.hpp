@@ -402,8 +402,9 @@ __device__ __forceinline__ uint32_t p_word(const PKind& k, uint32_t a, uint32_t 
 // 2 skip snapshot stores, 4 skip normalization, 8 no P broadcast, 16 never run checked bodies,
 // 32 broadcast P with DPP row_newbcast, 64 ds_swizzle issued 4 columns ahead behind a
 // scheduling barrier, 128 the v3 column (packed adds + v_mov_dpp), 256 SDWA pad shifts,
-// 512 the shifted-pad 32-bit-add column (column4, the previous default).  128/256/512 are
-// exact (other layouts), the rest are timing-only.
+// 512 the shifted-pad 32-bit-add column (column4, the previous default), 1024 no soft fetch
+// (every body reuses the first body's soft values).  128/256/512 are exact (other layouts),
+// the rest are timing-only.
 template <int CR, int DBG = 0>
 struct Packet {
   using RT = Rate<CR>;
@@ -492,7 +493,7 @@ __device__ __forceinline__ uint32_t soft_off(uint32_t j) {
 }
 
 template <int CR, int DBG>
-__device__ void run_rows(const uint8_t* __restrict__ sp, uint32_t n, Row& R, const Consts& K, uint32_t l,
+__device__ void run_rows(const uint8_t* __restrict__ soft, int64_t so, uint32_t n, Row& R, const Consts& K, uint32_t l,
                          uint32_t rib, uint8_t* ring_block, uint8_t* __restrict__ out, uint32_t ooff) {
   using RT = Rate<CR>;
   const uint32_t p0 = pos_of(l, 0, 0), p1 = pos_of(l, 0, 1), p2 = pos_of(l, 1, 0), p3 = pos_of(l, 1, 1);
@@ -503,25 +504,43 @@ __device__ void run_rows(const uint8_t* __restrict__ sp, uint32_t n, Row& R, con
   const uint32_t j1 = l, j2 = 16u + (l & 7u);
   const uint32_t o1 = soft_off<CR>(j1), o2 = soft_off<CR>(j2);
   const uint32_t r1 = j1 % RT::steps, r2 = j2 % RT::steps;
-  // Soft values past the input are clamped to its last byte: the columns they feed lie
-  // beyond R.cols and never reach an output byte.  Unconditional loads (no exec branches)
-  // let the compiler wait for exactly the previous body's loads, not the prefetch.
-  const uint32_t last = n ? n - 1u : 0u;               // rows with no input read byte 0 (harmless)
-  auto fetch = [&](uint32_t base, uint32_t o, uint32_t r, uint32_t& a, uint32_t& b) {
-    const uint32_t i = min(base + o, last);
-    a = sp[i];
-    b = sp[min(i + 1u, last)];                         // used by full columns only (PKind.Mb)
-  };
   const PKind k1 = p_kind(r1), k2 = p_kind(r2);
+  // Soft values by buffer loads: one wave-uniform descriptor over the rows' soft windows,
+  // advanced by the scalar unit every body, and a per-lane byte offset that never changes
+  // (row offset + column offset; b at offset:1).  Reads past the furthest row's last soft
+  // value fall outside the descriptor and return 0; reads past a row's own end read its
+  // neighbour's values, which feed only columns beyond R.cols.  The rows of a wave must lie
+  // within 4 GiB of soft values (zrx_viterbi_dev documents the limit; rows of a wave that
+  // break it report -1 bits).
+  const int64_t lo_me = R.live ? so : INT64_MAX, hi_me = R.live ? so + (int64_t)n : INT64_MIN;
+  auto rl64 = [](int64_t v, int lane) {
+    return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), lane) << 32) |
+                     (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane));
+  };
+  const int64_t lo_w = min(min(rl64(lo_me, 0), rl64(lo_me, 16)), min(rl64(lo_me, 32), rl64(lo_me, 48)));
+  const int64_t hi_w = max(max(rl64(hi_me, 0), rl64(hi_me, 16)), max(rl64(hi_me, 32), rl64(hi_me, 48)));
+  if (hi_w - lo_w > (int64_t)0xFFFFFF00) {
+    if (R.live) R.nbytes = 0xFFFFFFFFu;
+    return;
+  }
+  const uint32_t rel = R.live ? (uint32_t)(so - lo_w) : 0u;
+  const uint32_t v1 = rel + o1, v2 = rel + o2;
+  auto fetch = [&](uint32_t base, uint32_t& a1_, uint32_t& b1_, uint32_t& a2_, uint32_t& b2_) {
+    const int64_t left = hi_w - lo_w - (int64_t)base;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(soft + lo_w + base), (short)0, (int)(uint32_t)(left > 0 ? left : 0), 0x00020000);
+    a1_ = __builtin_amdgcn_raw_buffer_load_b8(rs, (int)v1, 0, 0);
+    b1_ = __builtin_amdgcn_raw_buffer_load_b8(rs, (int)v1 + 1, 0, 0);
+    a2_ = __builtin_amdgcn_raw_buffer_load_b8(rs, (int)v2, 0, 0);
+    b2_ = __builtin_amdgcn_raw_buffer_load_b8(rs, (int)v2 + 1, 0, 0);
+  };
   uint32_t a1, b1, a2, b2;
-  fetch(0, o1, r1, a1, b1);
-  fetch(0, o2, r2, a2, b2);
+  fetch(0, a1, b1, a2, b2);
   uint32_t s_next = wave_min_rows(R.next);
   uint32_t slot = 0;                                   // first slot of this body (3 per body)
   for (uint32_t tr0 = 0, base = 0; __builtin_amdgcn_ballot_w64(R.live) != 0; tr0 += 24, base += RT::chunk) {
     const uint32_t Pa = p_word(k1, a1, b1), Pb = p_word(k2, a2, b2);
-    fetch(base + RT::chunk, o1, r1, a1, b1);           // next body's soft values (latency hidden)
-    fetch(base + RT::chunk, o2, r2, a2, b2);
+    if constexpr ((DBG & 1024) == 0) fetch(base + RT::chunk, a1, b1, a2, b2);   // next body (latency hidden)
     pk.ring = ring_block + slot * kSlotBytes;
     if ((DBG & 16) || s_next > tr0 + 24)
       pk.template body<false>(M0, M1, Pa, Pb, tr0, s_next, std::make_integer_sequence<int, 24>{});
@@ -572,7 +591,6 @@ __global__ __launch_bounds__(256, 4) void k_viterbi3(const uint8_t* __restrict__
   const uint32_t cols = valid && n > 0 && cr >= 0 && cr <= 2 ? (uint32_t)(n / (cr == 0 ? 2 : cr == 1 ? 3 : 4)) * (uint32_t)(cr + 1) : 0u;
   v3::Consts K;
   v3::make_consts(K, l, rib);
-  const uint8_t* sp = soft + so;
   // output bytes are addressed as out + 32-bit offset (one uniform base for the whole wave)
   uint8_t* obase = out + (oo & ~(int64_t)0xFFFFFFFF);
   const uint32_t ooff = (uint32_t)(oo & 0xFFFFFFFF);
@@ -590,12 +608,12 @@ __global__ __launch_bounds__(256, 4) void k_viterbi3(const uint8_t* __restrict__
     Rr.pM0 = Rr.pM1 = Rr.fM0 = Rr.fM1 = 0;
     Rr.nbytes = 0;
     Rr.next = v3::row_next(Rr);
-    if (rate == 0) v3::run_rows<0, DBG>(sp, (uint32_t)max(n, 0), Rr, K, l, rib, ring, obase, ooff);
-    else if (rate == 1) v3::run_rows<1, DBG>(sp, (uint32_t)max(n, 0), Rr, K, l, rib, ring, obase, ooff);
-    else v3::run_rows<2, DBG>(sp, (uint32_t)max(n, 0), Rr, K, l, rib, ring, obase, ooff);
+    if (rate == 0) v3::run_rows<0, DBG>(soft, so, (uint32_t)max(n, 0), Rr, K, l, rib, ring, obase, ooff);
+    else if (rate == 1) v3::run_rows<1, DBG>(soft, so, (uint32_t)max(n, 0), Rr, K, l, rib, ring, obase, ooff);
+    else v3::run_rows<2, DBG>(soft, so, (uint32_t)max(n, 0), Rr, K, l, rib, ring, obase, ooff);
     if (mine) nbytes = Rr.nbytes;
   }
-  if (valid && l == 0) out_bits[p] = (int32_t)(nbytes * 8u);
+  if (valid && l == 0) out_bits[p] = nbytes == 0xFFFFFFFFu ? -1 : (int32_t)(nbytes * 8u);
 }
 
 // Packet order for k_viterbi3 over a mixed batch (BASELINE config 5): by code rate, then by
