@@ -292,14 +292,58 @@ __device__ __forceinline__ void events(Row& R, uint32_t tr, uint32_t M0, uint32_
   }
 }
 
+// Deferred tail of a traceback walk shared by the rows of a wave (same window).  The last D
+// output bytes of the window (D = 24, 20 or 12) are walked one step per column of the next
+// body (Packet::col, columns 0 .. D-1), where each step's LDS latency hides behind the
+// column's work: the step packs the byte read by the previous column into a dword, moves
+// the ring index on and issues the next read; every fourth step stores the dword with a
+// buffer store (rows that do not own the window store out of range, i.e. nothing).  The
+// slot base steps back on the scalar unit.  we = D (0: nothing deferred).
+struct Walk {
+  int we;                         // wave-uniform
+  uint32_t A;                     // wave-uniform: slot of the pending read
+  uint32_t ix, b, acc, voff;      // per lane: ring index (row offset included), pending byte, dword, store offset
+  uint64_t ob;                    // wave-uniform: output base the store offsets are relative to
+};
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t walk_rsrc(const Walk& W) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)W.ob, (short)0, 0x7FFFFFFF, 0x00020000);
+}
+// The setup runs in a branch whose join the divergence analysis cannot prove uniform; the
+// scalar fields are uniform by construction, so they are re-read as such.
+__device__ __forceinline__ void walk_uniform(Walk& W) {
+  W.we = __builtin_amdgcn_readfirstlane(W.we);
+  W.A = (uint32_t)__builtin_amdgcn_readfirstlane((int)W.A);
+  W.ob = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(W.ob >> 32)) << 32) |
+         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)W.ob);
+}
+
+// The deferred tail without a following body (the rows stopped): the same steps back to back.
+__device__ __forceinline__ void walk_finish(Walk& W, const uint8_t* ring0, uint32_t rb) {
+  constexpr uint32_t span = (uint32_t)kRing * kSlotBytes;
+  for (int J = 0; J < W.we; J++) {
+    const uint32_t b = W.b;
+    W.acc = (W.acc << 8) | b;
+    W.ix = (b & 63u) | rb;
+    W.A = W.A == 0u ? span - (uint32_t)kSlotBytes : W.A - (uint32_t)kSlotBytes;
+    if (J < W.we - 1) W.b = ring0[W.A + W.ix];
+    if ((J & 3) == 3)
+      __builtin_amdgcn_raw_buffer_store_b32(W.acc, walk_rsrc(W), (int)(W.voff + (uint32_t)(W.we - 1 - J)), 0, 0);
+  }
+  W.we = 0;
+}
+
 // Traceback of one window for the rows with `due` set: argmin over the row (all lanes),
 // then one lane per row walks the snapshot ring and writes the window's bytes.  The walk is
 // a chain of dependent LDS reads (state -> byte -> state 8 columns back), so the loop body
 // keeps only the read, the bit reversal and the address add on that chain.
-template <bool V5>
+// DEFER (partial windows): rows sharing a window leave the window's last 24 or 16 output
+// bytes to the next body's columns (W); tr0 is the first column of the body that raised the
+// event.
+template <bool V5, bool DEFER = false>
 __device__ __forceinline__ void traceback(bool due, uint32_t M0, uint32_t M1, uint32_t T, uint32_t cnt,
                                           uint32_t look, uint32_t l, uint32_t rib, const uint8_t* ring,
-                                          uint8_t* __restrict__ out, uint32_t ooff, uint32_t& nbytes) {
+                                          uint8_t* __restrict__ out, uint32_t ooff, uint32_t& nbytes,
+                                          Walk* W = nullptr, uint32_t tr0 = 0) {
   const uint32_t ph = T % 6u;
   uint32_t best = 0xFFFFFFFFu;
 #pragma unroll
@@ -340,14 +384,54 @@ __device__ __forceinline__ void traceback(bool due, uint32_t M0, uint32_t M1, ui
   const uint32_t C0f = (uint32_t)__builtin_amdgcn_readlane((int)C0, first);
   const uint32_t chf = (uint32_t)__builtin_amdgcn_readlane((int)c_hi, first);
   const uint32_t nof = (uint32_t)__builtin_amdgcn_readlane((int)nout, first);
-  const bool uni = __builtin_amdgcn_ballot_w64(walker && (C0 != C0f || c_hi != chf || nout != nof)) == 0;
-  if (!walker) return;
+  const uint64_t ob_me = (uint64_t)(uintptr_t)out;    // rows of one window share the 4 GiB output base
+  const uint64_t obf = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(ob_me >> 32), first) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ob_me, first);
+  const bool uni = __builtin_amdgcn_ballot_w64(walker && (C0 != C0f || c_hi != chf || nout != nof ||
+                                                          ob_me != obf)) == 0;
   const uint32_t rb = rib * 64u;
   uint32_t ix = rb + (__builtin_bitreverse32((Z >> (T - C0)) & 63u) >> 26);   // ring index = rev6(state)
+  // Deferral: window step i reads slot C0 - i.  The next body's snapshot k (k = 0, 1, 2, at
+  // the end of its column 5 + 8k) overwrites slot C0 - (38 - k - s), s = slots between C0
+  // and this body's newest snapshot (tr0 + 22); deferred step m runs first thing in column m
+  // and issues the read of window step nl + 32 - D + m + 1.  That read must precede the
+  // overwrite of its slot whenever the slot is part of the window (38 - k - s <= nl + 31):
+  // D <= 9k + s + nl, so D = 24 unless (s, nl) = (2, 3) or (3, 2) (D = 20) or (3, 3) (D = 12).
+  const uint32_t s = (tr0 + 22u - C0f) >> 3;
+  const uint32_t nlf = (C0f - chf) >> 3;
+  const uint32_t Dw = s + nlf <= 4u ? 24u : (s + nlf == 5u ? 20u : (s + nlf == 6u ? 12u : 0u));
+  const uint32_t D = (DEFER && uni && nof == 32u) ? Dw : 0u;
   uint8_t* op = out + ooff + ((c_hi - 14u) >> 3);      // output byte of block c_hi, newest first
+  auto prevS = [](uint32_t x) { return x == 0u ? span - (uint32_t)kSlotBytes : x - (uint32_t)kSlotBytes; };
+  if (DEFER && D != 0u) {                              // wave-uniform branch: every lane runs the walk
+    uint32_t A = (((C0f - 6u) >> 3) % (uint32_t)kRing) * kSlotBytes;
+    const uint32_t nl = (C0f - chf) >> 3;
+    for (uint32_t i = 0; i < nl; i++) {
+      ix = (ring[A + ix] & 63u) | rb;
+      A = prevS(A);
+    }
+    for (uint32_t i = 0; i < 32u - D; i++) {           // the window's head: bytes 31 .. D
+      const uint32_t b = ring[A + ix];
+      if (walker) *op = (uint8_t)b;
+      op--;
+      ix = (b & 63u) | rb;
+      A = prevS(A);
+    }
+    W->we = (int)D;
+    W->A = A;
+    W->ix = ix;
+    W->acc = 0;
+    W->b = ring[A + ix];                               // the first deferred step's read
+    W->ob = obf;
+    // byte 0 of the window (its lowest address) relative to the shared base; other lanes
+    // store out of range
+    W->voff = walker ? (uint32_t)((uint64_t)(uintptr_t)(op + 1 - D) - obf) : 0x80000000u;
+    if (walker) nbytes = max(nbytes, ((chf - 14u) >> 3) + 1u);
+    return;
+  }
+  if (!walker) return;
   if (uni) {
     uint32_t A = (((C0f - 6u) >> 3) % (uint32_t)kRing) * kSlotBytes;   // uniform slot base
-    auto prevS = [](uint32_t x) { return x == 0u ? span - (uint32_t)kSlotBytes : x - (uint32_t)kSlotBytes; };
     const uint32_t nl = (C0f - chf) >> 3;
     for (uint32_t i = 0; i < nl; i++) {                // lookahead blocks: state only
       ix = (ring[A + ix] & 63u) | rb;
@@ -412,7 +496,9 @@ struct Packet {
   const Consts& K;
   Row& R;
   uint32_t l, rib;
-  uint8_t* ring;
+  uint8_t* ring;                                       // this body's first snapshot slot
+  uint8_t* ring0;                                      // the block's ring (slot 0)
+  Walk* W;                                             // deferred traceback tail (WS >= 0 bodies)
 
   template <int J>
   static __device__ __forceinline__ uint32_t bcast(uint32_t Pa, uint32_t Pb) {   // P word of body column J
@@ -421,9 +507,22 @@ struct Packet {
     else
       return (uint32_t)__builtin_amdgcn_ds_swizzle((int)(J < 16 ? Pa : Pb), ((J & 15) << 5) | 0x10);
   }
-  template <int J, bool CHECKED>
+  // One deferred traceback step (branch-free; see Walk).
+  template <int J, int WE>
+  __device__ __forceinline__ void walk_col() {
+    constexpr uint32_t span = (uint32_t)kRing * kSlotBytes;
+    const uint32_t b = W->b;
+    W->acc = (W->acc << 8) | b;
+    W->ix = (b & 63u) | (rib * 64u);
+    W->A = W->A == 0u ? span - (uint32_t)kSlotBytes : W->A - (uint32_t)kSlotBytes;
+    if constexpr (J < WE - 1) W->b = ring0[W->A + W->ix];
+    if constexpr (J % 4 == 3)                          // bytes D-1-J .. D+2-J of the window
+      __builtin_amdgcn_raw_buffer_store_b32(W->acc, walk_rsrc(*W), (int)(W->voff + (uint32_t)(WE - 1 - J)), 0, 0);
+  }
+  template <int J, bool CHECKED, int WE>
   __device__ __forceinline__ void col(uint32_t& M0, uint32_t& M1, uint32_t (&Pq)[4], uint32_t Pa, uint32_t Pb,
                                       uint32_t tr0, uint32_t& s_next) {
+    if constexpr (J < WE) walk_col<J, WE>();
     uint32_t P;
     if constexpr ((DBG & 8) != 0) {
       P = J < 16 ? Pa : Pb;
@@ -473,14 +572,14 @@ struct Packet {
       }
     }
   }
-  template <bool CHECKED, int... J>
+  template <bool CHECKED, int WE, int... J>
   __device__ __forceinline__ void body(uint32_t& M0, uint32_t& M1, uint32_t Pa, uint32_t Pb, uint32_t tr0,
                                        uint32_t& s_next, std::integer_sequence<int, J...>) {
     uint32_t Pq[4] = {0, 0, 0, 0};
     if constexpr (!(DBG & 40)) {
       Pq[0] = bcast<0>(Pa, Pb); Pq[1] = bcast<1>(Pa, Pb); Pq[2] = bcast<2>(Pa, Pb); Pq[3] = bcast<3>(Pa, Pb);
     }
-    (col<J, CHECKED>(M0, M1, Pq, Pa, Pb, tr0, s_next), ...);
+    (col<J, CHECKED, WE>(M0, M1, Pq, Pa, Pb, tr0, s_next), ...);
   }
 };
 
@@ -493,13 +592,19 @@ __device__ __forceinline__ uint32_t soft_off(uint32_t j) {
 }
 
 template <int CR, int DBG>
-__device__ void run_rows(const uint8_t* __restrict__ soft, int64_t so, uint32_t n, Row& R, const Consts& K, uint32_t l,
+__device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64_t so, uint32_t n, Row& R, const Consts& K, uint32_t l,
                          uint32_t rib, uint8_t* ring_block, uint8_t* __restrict__ out, uint32_t ooff) {
   using RT = Rate<CR>;
   const uint32_t p0 = pos_of(l, 0, 0), p1 = pos_of(l, 0, 1), p2 = pos_of(l, 1, 0), p3 = pos_of(l, 1, 1);
   uint32_t M0 = ((p1 ? 48u : 0u) << 24) | ((p0 ? 48u : 0u) << 8);   // ALL_INIT0 (viterbilut.h:74-82)
   uint32_t M1 = ((p3 ? 48u : 0u) << 24) | ((p2 ? 48u : 0u) << 8);
-  Packet<CR, DBG> pk{K, R, l, rib, ring_block};
+  Walk W;
+  W.we = 0;
+  W.A = 0;
+  W.ix = W.b = W.acc = 0;
+  W.voff = 0x80000000u;
+  W.ob = (uint64_t)(uintptr_t)out;
+  Packet<CR, DBG> pk{K, R, l, rib, ring_block, ring_block, &W};
   // this lane builds the P words of body columns j1 = l and j2 = 16 + l (l < 8)
   const uint32_t j1 = l, j2 = 16u + (l & 7u);
   const uint32_t o1 = soft_off<CR>(j1), o2 = soft_off<CR>(j2);
@@ -538,17 +643,40 @@ __device__ void run_rows(const uint8_t* __restrict__ soft, int64_t so, uint32_t 
   fetch(0, a1, b1, a2, b2);
   uint32_t s_next = wave_min_rows(R.next);
   uint32_t slot = 0;                                   // first slot of this body (3 per body)
-  for (uint32_t tr0 = 0, base = 0; __builtin_amdgcn_ballot_w64(R.live) != 0; tr0 += 24, base += RT::chunk) {
-    const uint32_t Pa = p_word(k1, a1, b1), Pb = p_word(k2, a2, b2);
-    if constexpr ((DBG & 1024) == 0) fetch(base + RT::chunk, a1, b1, a2, b2);   // next body (latency hidden)
-    pk.ring = ring_block + slot * kSlotBytes;
-    if ((DBG & 16) || s_next > tr0 + 24)
-      pk.template body<false>(M0, M1, Pa, Pb, tr0, s_next, std::make_integer_sequence<int, 24>{});
-    else
-      pk.template body<true>(M0, M1, Pa, Pb, tr0, s_next, std::make_integer_sequence<int, 24>{});
+  uint32_t tr0 = 0, base = 0;
+  constexpr auto cols24 = std::make_integer_sequence<int, 24>{};
+  auto next_body = [&]() {
     slot = slot + 3 == kRing ? 0 : slot + 3;
+    tr0 += 24;
+    base += RT::chunk;
+  };
+  while (__builtin_amdgcn_ballot_w64(R.live) != 0) {
+    // The hot loop: bodies with no event due, no deferred walk, nothing else on this path
+    // (its own loop, so the register allocator keeps the loop-carried values in place).
+    while ((DBG & 16) || (s_next > tr0 + 24 && s_next != kNever)) {
+      const uint32_t Pa = p_word(k1, a1, b1), Pb = p_word(k2, a2, b2);
+      if constexpr ((DBG & 1024) == 0) fetch(base + RT::chunk, a1, b1, a2, b2);   // next body (latency hidden)
+      pk.ring = ring_block + slot * kSlotBytes;
+      pk.template body<false, 0>(M0, M1, Pa, Pb, tr0, s_next, cols24);
+      next_body();
+      if constexpr ((DBG & 16) != 0) {                 // no events: stop at the input's end
+        if (tr0 >= R.cols) R.live = false;
+        if (__builtin_amdgcn_ballot_w64(R.live) == 0) break;
+      }
+    }
+    if constexpr ((DBG & 16) != 0) break;
+    if (s_next == kNever) break;                       // every row is done
+    // A body with an event due: checked, then the tracebacks it raised.
+    {
+      const uint32_t Pa = p_word(k1, a1, b1), Pb = p_word(k2, a2, b2);
+      if constexpr ((DBG & 1024) == 0) fetch(base + RT::chunk, a1, b1, a2, b2);
+      pk.ring = ring_block + slot * kSlotBytes;
+      pk.template body<true, 0>(M0, M1, Pa, Pb, tr0, s_next, cols24);
+    }
     if ((DBG & 1) == 0 && __builtin_amdgcn_ballot_w64(R.ppend) != 0) {
-      traceback<Packet<CR, DBG>::V5>(R.ppend, R.pM0, R.pM1, R.pT, 256u, R.plook, l, rib, ring_block, out, ooff, R.nbytes);
+      traceback<Packet<CR, DBG>::V5, Packet<CR, DBG>::V5>(R.ppend, R.pM0, R.pM1, R.pT, 256u, R.plook, l, rib,
+                                                           ring_block, out, ooff, R.nbytes, &W, tr0);
+      walk_uniform(W);
       R.ppend = false;
     }
     if ((DBG & 1) == 0 && __builtin_amdgcn_ballot_w64(R.fpend) != 0) {
@@ -556,10 +684,26 @@ __device__ void run_rows(const uint8_t* __restrict__ soft, int64_t so, uint32_t 
       R.fpend = false;
     }
     if constexpr ((DBG & 1) != 0) R.ppend = R.fpend = false;
-    if constexpr ((DBG & 16) != 0) {                   // no events: stop at the input's end
-      if (tr0 + 24 >= R.cols) R.live = false;
+    next_body();
+    // The deferred tail of a window runs in the next body's columns (checked: rare).
+    if (W.we && __builtin_amdgcn_ballot_w64(R.live) != 0) {
+      const uint32_t Pa = p_word(k1, a1, b1), Pb = p_word(k2, a2, b2);
+      if constexpr ((DBG & 1024) == 0) fetch(base + RT::chunk, a1, b1, a2, b2);
+      pk.ring = ring_block + slot * kSlotBytes;
+      if (W.we == 24) pk.template body<true, 24>(M0, M1, Pa, Pb, tr0, s_next, cols24);
+      else if (W.we == 20) pk.template body<true, 20>(M0, M1, Pa, Pb, tr0, s_next, cols24);
+      else pk.template body<true, 12>(M0, M1, Pa, Pb, tr0, s_next, cols24);
+      W.we = 0;
+      if ((DBG & 1) == 0 && __builtin_amdgcn_ballot_w64(R.fpend) != 0) {   // (a partial window is 256 columns on)
+        traceback<Packet<CR, DBG>::V5>(R.fpend, R.fM0, R.fM1, R.fT, R.fcnt, R.flook, l, rib, ring_block, out, ooff,
+                                       R.nbytes);
+        R.fpend = false;
+      }
+      if constexpr ((DBG & 1) != 0) R.ppend = R.fpend = false;
+      next_body();
     }
   }
+  if (W.we) walk_finish(W, ring_block, rib * 64u);     // rows done before the deferred tail ran
 }
 
 }  // namespace v3
