@@ -292,13 +292,14 @@ __device__ __forceinline__ void events(Row& R, uint32_t tr, uint32_t M0, uint32_
   }
 }
 
-// Deferred tail of a traceback walk shared by the rows of a wave (same window).  The last D
-// output bytes of the window (D = 24, 20 or 12) are walked one step per column of the next
-// body (Packet::col, columns 0 .. D-1), where each step's LDS latency hides behind the
-// column's work: the step packs the byte read by the previous column into a dword, moves
-// the ring index on and issues the next read; every fourth step stores the dword with a
-// buffer store (rows that do not own the window store out of range, i.e. nothing).  The
-// slot base steps back on the scalar unit.  we = D (0: nothing deferred).
+// A traceback walk shared by the rows of a wave (same window), deferred to the next body:
+// its nl + 32 steps (nl lookahead blocks, then the window's 32 output bytes, newest first)
+// run inside that body's columns, two per column in columns 0..11 and one per column after
+// (Packet::walk_col), so each step's LDS latency hides behind column work.  A step packs the
+// byte read before into a dword, moves the ring index on and issues the next read; every
+// fourth output byte stores the dword with a buffer store (rows that do not own the window
+// store out of range, i.e. nothing).  The slot base steps back on the scalar unit.
+// we = nl (0: nothing deferred).
 struct Walk {
   int we;                         // wave-uniform
   uint32_t A;                     // wave-uniform: slot of the pending read
@@ -317,18 +318,22 @@ __device__ __forceinline__ void walk_uniform(Walk& W) {
          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)W.ob);
 }
 
-// The deferred tail without a following body (the rows stopped): the same steps back to back.
-__device__ __forceinline__ void walk_finish(Walk& W, const uint8_t* ring0, uint32_t rb) {
+// One walk step t (compile-time when called from the body columns).
+template <class I>
+__device__ __forceinline__ void walk_stepk(Walk& W, I t, uint32_t nl, const uint8_t* ring0, uint32_t rb) {
   constexpr uint32_t span = (uint32_t)kRing * kSlotBytes;
-  for (int J = 0; J < W.we; J++) {
-    const uint32_t b = W.b;
-    W.acc = (W.acc << 8) | b;
-    W.ix = (b & 63u) | rb;
-    W.A = W.A == 0u ? span - (uint32_t)kSlotBytes : W.A - (uint32_t)kSlotBytes;
-    if (J < W.we - 1) W.b = ring0[W.A + W.ix];
-    if ((J & 3) == 3)
-      __builtin_amdgcn_raw_buffer_store_b32(W.acc, walk_rsrc(W), (int)(W.voff + (uint32_t)(W.we - 1 - J)), 0, 0);
-  }
+  const uint32_t b = W.b;
+  W.acc = (W.acc << 8) | b;                            // lookahead bytes leave before the first store
+  W.ix = (b & 63u) | rb;
+  W.A = W.A == 0u ? span - (uint32_t)kSlotBytes : W.A - (uint32_t)kSlotBytes;
+  if (t + 1 < nl + 32u) W.b = ring0[W.A + W.ix];
+  if (t >= nl && ((t - nl) & 3u) == 3u)                // output bytes 31-o .. 34-o, o = t - nl
+    __builtin_amdgcn_raw_buffer_store_b32(W.acc, walk_rsrc(W), (int)(W.voff + 31u - (t - nl)), 0, 0);
+}
+// The deferred walk without a following body (the rows stopped): its steps back to back.
+__device__ __forceinline__ void walk_finish(Walk& W, const uint8_t* ring0, uint32_t rb) {
+  const uint32_t nl = (uint32_t)W.we;
+  for (uint32_t t = 0; t < nl + 32u; t++) walk_stepk(W, t, nl, ring0, rb);
   W.we = 0;
 }
 
@@ -393,39 +398,24 @@ __device__ __forceinline__ void traceback(bool due, uint32_t M0, uint32_t M1, ui
   uint32_t ix = rb + (__builtin_bitreverse32((Z >> (T - C0)) & 63u) >> 26);   // ring index = rev6(state)
   // Deferral: window step i reads slot C0 - i.  The next body's snapshot k (k = 0, 1, 2, at
   // the end of its column 5 + 8k) overwrites slot C0 - (38 - k - s), s = slots between C0
-  // and this body's newest snapshot (tr0 + 22); deferred step m runs first thing in column m
-  // and issues the read of window step nl + 32 - D + m + 1.  That read must precede the
-  // overwrite of its slot whenever the slot is part of the window (38 - k - s <= nl + 31):
-  // D <= 9k + s + nl, so D = 24 unless (s, nl) = (2, 3) or (3, 2) (D = 20) or (3, 3) (D = 12).
+  // and this body's newest snapshot (tr0 + 22).  With two steps per column in columns 0..11
+  // and one after, the read of step i is issued in column i / 2 (i <= 24) or i - 12: before
+  // every overwrite of a window slot when s <= 2 (s = 3 only occurs with T in a body's first
+  // six columns; those windows walk now).
   const uint32_t s = (tr0 + 22u - C0f) >> 3;
   const uint32_t nlf = (C0f - chf) >> 3;
-  const uint32_t Dw = s + nlf <= 4u ? 24u : (s + nlf == 5u ? 20u : (s + nlf == 6u ? 12u : 0u));
-  const uint32_t D = (DEFER && uni && nof == 32u) ? Dw : 0u;
   uint8_t* op = out + ooff + ((c_hi - 14u) >> 3);      // output byte of block c_hi, newest first
   auto prevS = [](uint32_t x) { return x == 0u ? span - (uint32_t)kSlotBytes : x - (uint32_t)kSlotBytes; };
-  if (DEFER && D != 0u) {                              // wave-uniform branch: every lane runs the walk
-    uint32_t A = (((C0f - 6u) >> 3) % (uint32_t)kRing) * kSlotBytes;
-    const uint32_t nl = (C0f - chf) >> 3;
-    for (uint32_t i = 0; i < nl; i++) {
-      ix = (ring[A + ix] & 63u) | rb;
-      A = prevS(A);
-    }
-    for (uint32_t i = 0; i < 32u - D; i++) {           // the window's head: bytes 31 .. D
-      const uint32_t b = ring[A + ix];
-      if (walker) *op = (uint8_t)b;
-      op--;
-      ix = (b & 63u) | rb;
-      A = prevS(A);
-    }
-    W->we = (int)D;
-    W->A = A;
+  if (DEFER && uni && nof == 32u && s <= 2u && (nlf == 2u || nlf == 3u)) {   // wave-uniform: every lane
+    W->we = (int)nlf;
+    W->A = (((C0f - 6u) >> 3) % (uint32_t)kRing) * kSlotBytes;
     W->ix = ix;
     W->acc = 0;
-    W->b = ring[A + ix];                               // the first deferred step's read
+    W->b = ring[W->A + ix];                            // step 0's read
     W->ob = obf;
     // byte 0 of the window (its lowest address) relative to the shared base; other lanes
     // store out of range
-    W->voff = walker ? (uint32_t)((uint64_t)(uintptr_t)(op + 1 - D) - obf) : 0x80000000u;
+    W->voff = walker ? (uint32_t)((uint64_t)(uintptr_t)(op - 31) - obf) : 0x80000000u;
     if (walker) nbytes = max(nbytes, ((chf - 14u) >> 3) + 1u);
     return;
   }
@@ -507,22 +497,21 @@ struct Packet {
     else
       return (uint32_t)__builtin_amdgcn_ds_swizzle((int)(J < 16 ? Pa : Pb), ((J & 15) << 5) | 0x10);
   }
-  // One deferred traceback step (branch-free; see Walk).
-  template <int J, int WE>
+  // The deferred traceback steps of column J (branch-free; see Walk): steps 2J, 2J + 1 in
+  // columns 0..11, step J + 12 after, NL + 32 steps in all.
+  template <int J, int NL>
   __device__ __forceinline__ void walk_col() {
-    constexpr uint32_t span = (uint32_t)kRing * kSlotBytes;
-    const uint32_t b = W->b;
-    W->acc = (W->acc << 8) | b;
-    W->ix = (b & 63u) | (rib * 64u);
-    W->A = W->A == 0u ? span - (uint32_t)kSlotBytes : W->A - (uint32_t)kSlotBytes;
-    if constexpr (J < WE - 1) W->b = ring0[W->A + W->ix];
-    if constexpr (J % 4 == 3)                          // bytes D-1-J .. D+2-J of the window
-      __builtin_amdgcn_raw_buffer_store_b32(W->acc, walk_rsrc(*W), (int)(W->voff + (uint32_t)(WE - 1 - J)), 0, 0);
+    if constexpr (J < 12) {
+      walk_stepk(*W, (uint32_t)(2 * J), (uint32_t)NL, ring0, rib * 64u);
+      walk_stepk(*W, (uint32_t)(2 * J + 1), (uint32_t)NL, ring0, rib * 64u);
+    } else if constexpr (J + 12 < NL + 32) {
+      walk_stepk(*W, (uint32_t)(J + 12), (uint32_t)NL, ring0, rib * 64u);
+    }
   }
   template <int J, bool CHECKED, int WE>
   __device__ __forceinline__ void col(uint32_t& M0, uint32_t& M1, uint32_t (&Pq)[4], uint32_t Pa, uint32_t Pb,
                                       uint32_t tr0, uint32_t& s_next) {
-    if constexpr (J < WE) walk_col<J, WE>();
+    if constexpr (WE > 0) walk_col<J, WE>();
     uint32_t P;
     if constexpr ((DBG & 8) != 0) {
       P = J < 16 ? Pa : Pb;
@@ -685,14 +674,13 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
     }
     if constexpr ((DBG & 1) != 0) R.ppend = R.fpend = false;
     next_body();
-    // The deferred tail of a window runs in the next body's columns (checked: rare).
+    // A deferred traceback walk runs in the next body's columns (checked: rare).
     if (W.we && __builtin_amdgcn_ballot_w64(R.live) != 0) {
       const uint32_t Pa = p_word(k1, a1, b1), Pb = p_word(k2, a2, b2);
       if constexpr ((DBG & 1024) == 0) fetch(base + RT::chunk, a1, b1, a2, b2);
       pk.ring = ring_block + slot * kSlotBytes;
-      if (W.we == 24) pk.template body<true, 24>(M0, M1, Pa, Pb, tr0, s_next, cols24);
-      else if (W.we == 20) pk.template body<true, 20>(M0, M1, Pa, Pb, tr0, s_next, cols24);
-      else pk.template body<true, 12>(M0, M1, Pa, Pb, tr0, s_next, cols24);
+      if (W.we == 3) pk.template body<true, 3>(M0, M1, Pa, Pb, tr0, s_next, cols24);
+      else pk.template body<true, 2>(M0, M1, Pa, Pb, tr0, s_next, cols24);
       W.we = 0;
       if ((DBG & 1) == 0 && __builtin_amdgcn_ballot_w64(R.fpend) != 0) {   // (a partial window is 256 columns on)
         traceback<Packet<CR, DBG>::V5>(R.fpend, R.fM0, R.fM1, R.fT, R.fcnt, R.flook, l, rib, ring_block, out, ooff,
