@@ -154,9 +154,8 @@ int zrx_get_timing(zrx_ctx* ctx, float* ms5);
 int zrx_fft64_dev(zrx_ctx* ctx, const struct complex16* d_in, struct complex16* d_out, int64_t nsym);
 
 /* d_params: 4 int32 per packet {frame_len, code_rate, soft_len, 0}; d_soft_off, d_out_off:
- * int64 byte offsets per packet; d_out_bits: int32 per packet (bits written).  The soft
- * values of one call must lie within 4 GiB of each other (split larger batches); a packet
- * decoded together with packets outside that window reports d_out_bits = -1. */
+ * int64 byte offsets per packet; d_out_bits: int32 per packet (bits written, or -1 for a
+ * packet of more than 4 GiB of soft values). */
 int zrx_viterbi_dev(zrx_ctx* ctx, const int8_t* d_soft, const int64_t* d_soft_off,
                     const int32_t* d_params, int npkts, uint8_t* d_out, const int64_t* d_out_off,
                     int32_t* d_out_bits);

@@ -251,6 +251,59 @@ def test_chain_truncated_and_bad_header(engine, oracle):
         assert info[i, 4] == 1
 
 
+def test_chain_mixed_distinct_large(engine, oracle):
+    """BASELINE config 5 shape at 2048 distinct packets (PSDU 64..4095 B, all 8 MCS, long
+    6 Mbps packets): every packet with a valid header passes its CRC with the transmitted
+    payload, and a sample equals the oracle packet for packet (mixed rates and lengths in a
+    wave, ordered rows, packed soft slots, shared and per-row traceback windows)."""
+    m = txgen.make_mixed_fast(2048, min_len=64, max_len=4095, sigma=3.0, seed=0xC5C5, device="cuda")
+    n = m["sym_off"].numel()
+    engine.reserve(n, m["max_nsym"])
+    pay, info = engine.rx(m["sym"], m["sym_off"], m["nsym"], m["max_nsym"])
+    pay, info = pay.cpu().numpy(), info.cpu().numpy()
+    valid = m["meta"][:, 2] <= 2048
+    assert (info[valid, 4] == 1).all(), np.nonzero(valid & (info[:, 4] != 1))[0][:10]
+    assert (info[~valid, 3] == 1).all()
+    for i in np.nonzero(valid)[0]:
+        assert (pay[i, :m["meta"][i, 2] - 4] == m["payload"][i]).all(), i
+    sample = 96
+    soff, sn = m["sym_off"][:sample].cpu().numpy(), m["nsym"][:sample].cpu().numpy()
+    opay, res = oracle.rx_batch_time(m["sym"][:int((soff + sn).max())].cpu().numpy(), soff, sn, nthreads=8)
+    for i, r in enumerate(res):
+        assert (info[i, 2], info[i, 4]) == (r["len"], r["crc_ok"]), i
+        if r["crc_ok"]:
+            assert (pay[i, :r["len"] - 4] == opay[i, :r["len"] - 4]).all(), i
+
+
+def test_viterbi_soft_spread_beyond_window():
+    """Rows of a wave whose soft values lie more than 4 GiB apart (device API) decode one at a
+    time, exactly."""
+    if torch.cuda.get_device_properties(0).total_memory < 12 << 30:
+        pytest.skip("needs > 12 GiB")
+    from tests.golden import synth
+    fl, cr = 300, 2
+    s = synth.viterbi_soft(cr, fl, 3, seed=41)
+    gap = (5 << 30) // 256 * 256
+    big = torch.zeros(gap + s.size + 4096, dtype=torch.int8, device="cuda")
+    srcs = torch.from_numpy(s).cuda()
+    big[:s.size] = srcs
+    big[gap:gap + s.size] = srcs
+    off = torch.tensor([0, gap, 0, gap], dtype=torch.int64, device="cuda")
+    params = torch.tensor([fl, cr, s.size, 0], dtype=torch.int32, device="cuda").repeat(4, 1).contiguous()
+    out = torch.zeros(4 * 512, dtype=torch.uint8, device="cuda")
+    oo = torch.arange(4, dtype=torch.int64, device="cuda") * 512
+    ob = torch.zeros(4, dtype=torch.int32, device="cuda")
+    e = RxEngine(0)
+    e.viterbi(big, off, params, out, oo, ob)
+    torch.cuda.synchronize()
+    e.close()
+    del big
+    exp = Z.viterbi_batch_decode(s, np.array([0, s.size], np.int32), np.array([fl], np.int32), np.array([cr], np.int16))[0][:fl]
+    o = out.cpu().numpy().reshape(4, 512)
+    assert (ob.cpu().numpy() == 8 * fl).all()
+    assert (o[:, :fl] == exp).all()
+
+
 def test_chain_nsym_beyond_reservation():
     """d_nsym larger than the reserved workspace: packets whose header needs more
     symbols than a soft slot holds get ZRX_PKT_OVERSIZE and nothing is written past their

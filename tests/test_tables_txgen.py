@@ -106,3 +106,18 @@ def test_txgen_mixed_decodes_in_oracle(oracle):
     for i, r in enumerate(res):
         assert r["crc_ok"] == 1 and (r["modulation"], r["coding"], r["len"]) == tuple(m["meta"][i])
         assert (pay[i, :r["len"] - 4] == m["payload"][i]).all()
+
+
+def test_txgen_mixed_fast_decodes_in_oracle(oracle):
+    """The vectorized config-5 generator: every packet distinct, all 8 MCS, header lengths up
+    to 4095 (those above 2048 are header errors the receiver must flag)."""
+    m = txgen.make_mixed_fast(48, min_len=64, max_len=2600, sigma=3.0, seed=9, chunk=5)
+    pay, res = oracle.rx_batch_time(m["sym"].numpy(), m["sym_off"].numpy(), m["nsym"].numpy(), nthreads=4)
+    assert len({p.tobytes() for p in m["payload"]}) == 48
+    assert len({int(x) for x in m["meta"][:, 0] * 4 + m["meta"][:, 1]}) >= 6
+    for i, r in enumerate(res):
+        if m["meta"][i, 2] > 2048:
+            assert r["crc_ok"] != 1
+            continue
+        assert r["crc_ok"] == 1 and (r["modulation"], r["coding"], r["len"]) == tuple(m["meta"][i])
+        assert (pay[i, :r["len"] - 4] == m["payload"][i]).all()

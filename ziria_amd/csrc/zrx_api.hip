@@ -49,7 +49,7 @@ struct zrx_ctx {
   uint32_t* sig_soft = nullptr;   // 48 B per packet
   int32_t* vparams = nullptr;     // 4 int32 per packet
   uint8_t* soft = nullptr;        // soft_stride B per packet
-  int64_t* soft_off = nullptr;    // p * soft_stride
+  int64_t* soft_off = nullptr;    // per packet, packed by soft_len (k_soft_scan)
   uint8_t* dec = nullptr;         // kDecStride B per packet
   int64_t* dec_off = nullptr;     // p * kDecStride
   int32_t* dec_bits = nullptr;
@@ -513,6 +513,7 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
                                                            (uint4*)c->sig_soft, chan, T);
   if (ev) ZRX_CHECK(hipEventRecord(ev[1], s));
   k_signal_vit<<<blocks(npkts, 4), 256, 0, s>>>(c->sig_soft, d_nsym, npkts, c->cap_nsym, c->vparams, d_info);
+  k_soft_scan<<<1, 1024, 0, s>>>(c->vparams, npkts, c->soft_off);   // packed soft slots
   if (ev) ZRX_CHECK(hipEventRecord(ev[2], s));
   // the Viterbi packet order needs only the headers: one block on the side stream, hidden
   // behind k_data_fft (a 1-block kernel costs ~20 us in line)

@@ -209,6 +209,35 @@ __global__ __launch_bounds__(256) void k_signal_vit(const uint32_t* __restrict__
   }
 }
 
+// Soft-value slots of the rx chain, packed by what each packet's header asks for:
+// off[p] = sum over q < p of soft_len(q) rounded up to 256 B (vparams[4q+2], k_signal_vit).
+// One 1024-thread block: a contiguous run of packets per thread, then a block scan.  Packed
+// slots keep a batch's soft values within the Viterbi's 4 GiB read window (a mixed batch
+// sized for its longest packet at 64-QAM would not be).
+__global__ __launch_bounds__(1024) void k_soft_scan(const int32_t* __restrict__ vparams, int npkts,
+                                                    int64_t* __restrict__ off) {
+  __shared__ int64_t wsum[16];
+  const int t = threadIdx.x;
+  const int per = (npkts + 1023) / 1024;
+  const int lo = min(t * per, npkts), hi = min(lo + per, npkts);
+  int64_t mine = 0;
+  for (int p = lo; p < hi; p++) mine += (int64_t)((vparams[4 * (int64_t)p + 2] + 255) & ~255);
+  int64_t inc = mine;                                  // inclusive scan inside the wave
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t u = __shfl_up(inc, o);
+    if ((t & 63) >= o) inc += u;
+  }
+  if ((t & 63) == 63) wsum[t >> 6] = inc;
+  __syncthreads();
+  int64_t base = inc - mine;
+  for (int w = 0; w < (t >> 6); w++) base += wsum[w];
+  for (int p = lo; p < hi; p++) {
+    off[p] = base;
+    base += (int64_t)((vparams[4 * (int64_t)p + 2] + 255) & ~255);
+  }
+}
+
 // ------------------------------------------------------------------ data symbols -> soft
 template <int MOD, bool EQ>
 __device__ __forceinline__ void data_fft_packet(const uint4* __restrict__ sym0, int need, int lane,

@@ -249,6 +249,13 @@ __device__ __forceinline__ void normalize(uint32_t& M0, uint32_t& M1) {
   M1 = w32(h2(M1) - h2(rep));
 }
 
+// 64-bit value of `lane` as a wave-uniform scalar
+__device__ __forceinline__ int64_t rl64(int64_t v, int lane) {
+  return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), lane) << 32) |
+                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane));
+}
+constexpr int64_t kSoftWindow = 0xFFFFFF00;           // span of one buffer window over soft values
+
 // Rate tables: steps per group, soft values per group, soft values per 24-column body.
 template <int CR> struct Rate;
 template <> struct Rate<0> { static constexpr int steps = 1, G = 2, chunk = 48; };   // 1/2
@@ -603,17 +610,12 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
   // advanced by the scalar unit every body, and a per-lane byte offset that never changes
   // (row offset + column offset; b at offset:1).  Reads past the furthest row's last soft
   // value fall outside the descriptor and return 0; reads past a row's own end read its
-  // neighbour's values, which feed only columns beyond R.cols.  The rows of a wave must lie
-  // within 4 GiB of soft values (zrx_viterbi_dev documents the limit; rows of a wave that
-  // break it report -1 bits).
+  // neighbour's values, which feed only columns beyond R.cols.  The caller (k_viterbi3)
+  // passes rows whose soft values lie within kSoftWindow of each other.
   const int64_t lo_me = R.live ? so : INT64_MAX, hi_me = R.live ? so + (int64_t)n : INT64_MIN;
-  auto rl64 = [](int64_t v, int lane) {
-    return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), lane) << 32) |
-                     (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane));
-  };
   const int64_t lo_w = min(min(rl64(lo_me, 0), rl64(lo_me, 16)), min(rl64(lo_me, 32), rl64(lo_me, 48)));
   const int64_t hi_w = max(max(rl64(hi_me, 0), rl64(hi_me, 16)), max(rl64(hi_me, 32), rl64(hi_me, 48)));
-  if (hi_w - lo_w > (int64_t)0xFFFFFF00) {
+  if (hi_w - lo_w > kSoftWindow) {                     // one row's soft values beyond 4 GiB: not decodable
     if (R.live) R.nbytes = 0xFFFFFFFFu;
     return;
   }
@@ -732,18 +734,29 @@ __global__ __launch_bounds__(256, 4) void k_viterbi3(const uint8_t* __restrict__
   for (int rate = 0; rate < 3; rate++) {
     const bool mine = cols > 0 && cr == rate;
     if (__builtin_amdgcn_ballot_w64(mine) == 0) continue;
-    v3::Row Rr;
-    Rr.ob = 0; Rr.end = (uint32_t)fl * 8u + 6u; Rr.cols = cols;
-    Rr.live = mine;
-    Rr.ppend = Rr.fpend = false;
-    Rr.pT = Rr.plook = Rr.fT = Rr.fcnt = Rr.flook = 0;
-    Rr.pM0 = Rr.pM1 = Rr.fM0 = Rr.fM1 = 0;
-    Rr.nbytes = 0;
-    Rr.next = v3::row_next(Rr);
-    if (rate == 0) v3::run_rows<0, DBG>(soft, so, (uint32_t)max(n, 0), Rr, K, l, rib, ring, obase, ooff);
-    else if (rate == 1) v3::run_rows<1, DBG>(soft, so, (uint32_t)max(n, 0), Rr, K, l, rib, ring, obase, ooff);
-    else v3::run_rows<2, DBG>(soft, so, (uint32_t)max(n, 0), Rr, K, l, rib, ring, obase, ooff);
-    if (mine) nbytes = Rr.nbytes;
+    // The soft values of a pass's rows are read through one 32-bit buffer window (run_rows);
+    // rows further apart than that run one at a time (correct, 4x the time; only batches
+    // with more than 4 GiB of soft values can get there).
+    const int64_t lo_me = mine ? so : INT64_MAX, hi_me = mine ? so + (int64_t)max(n, 0) : INT64_MIN;
+    const int64_t lo_w = min(min(v3::rl64(lo_me, 0), v3::rl64(lo_me, 16)), min(v3::rl64(lo_me, 32), v3::rl64(lo_me, 48)));
+    const int64_t hi_w = max(max(v3::rl64(hi_me, 0), v3::rl64(hi_me, 16)), max(v3::rl64(hi_me, 32), v3::rl64(hi_me, 48)));
+    const int passes = hi_w - lo_w > v3::kSoftWindow ? 4 : 1;
+    for (int q = 0; q < passes; q++) {
+      const bool mq = mine && (passes == 1 || (int)(rib & 3u) == q);
+      if (__builtin_amdgcn_ballot_w64(mq) == 0) continue;
+      v3::Row Rr;
+      Rr.ob = 0; Rr.end = (uint32_t)fl * 8u + 6u; Rr.cols = cols;
+      Rr.live = mq;
+      Rr.ppend = Rr.fpend = false;
+      Rr.pT = Rr.plook = Rr.fT = Rr.fcnt = Rr.flook = 0;
+      Rr.pM0 = Rr.pM1 = Rr.fM0 = Rr.fM1 = 0;
+      Rr.nbytes = 0;
+      Rr.next = v3::row_next(Rr);
+      if (rate == 0) v3::run_rows<0, DBG>(soft, so, (uint32_t)max(n, 0), Rr, K, l, rib, ring, obase, ooff);
+      else if (rate == 1) v3::run_rows<1, DBG>(soft, so, (uint32_t)max(n, 0), Rr, K, l, rib, ring, obase, ooff);
+      else v3::run_rows<2, DBG>(soft, so, (uint32_t)max(n, 0), Rr, K, l, rib, ring, obase, ooff);
+      if (mq) nbytes = Rr.nbytes;
+    }
   }
   if (valid && l == 0) out_bits[p] = nbytes == 0xFFFFFFFFu ? -1 : (int32_t)(nbytes * 8u);
 }

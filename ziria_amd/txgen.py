@@ -204,6 +204,78 @@ def make_batch(n, mod=3, coding=2, payload_len=1500, sigma=4.0, seed=0x5EED, dev
 MCS8 = [(0, 0), (0, 2), (1, 0), (1, 2), (2, 0), (2, 2), (3, 1), (3, 2)]
 
 
+def _signal_levels_batch(mod, coding, lengths, device):
+    """_signal_levels for many packets of one MCS: int64 [n, 48] BPSK levels."""
+    n = len(lengths)
+    h = np.zeros((n, 24), np.uint8)
+    code = RATE_NIBBLE[(mod, coding)]
+    h[:, 0:4] = [(code >> k) & 1 for k in range(4)]
+    L = np.asarray(lengths, np.int64)
+    h[:, 5:17] = (L[:, None] >> np.arange(12)) & 1
+    h[:, 17] ^= (h.sum(1) & 1).astype(np.uint8)
+    coded = _encode(torch.from_numpy(h).to(device), 0)
+    il = torch.empty_like(coded)
+    il[:, torch.from_numpy(interleave_perm(0)).to(device)] = coded
+    re, _ = _map(il[..., None], 0)
+    return re * UNIT[0]
+
+
+def make_mixed_fast(n, min_len=64, max_len=4095, sigma=4.0, seed=0x3C5, device="cpu", chunk=1024):
+    """BASELINE config 5 with n distinct packets, vectorized per MCS: the same transmitter and
+    channel as make_mixed (MCS uniform over the 8 rates, PSDU length uniform in [min_len,
+    max_len]), packets of one MCS built together on zero-padded bit arrays (the encoder is
+    causal, so a packet's own symbols do not depend on the padding).  Packet i's payload,
+    MCS and length come from one seeded generator in packet order; its noise from the
+    chunk it is built in."""
+    rng = np.random.default_rng(seed)
+    mcs = rng.integers(0, 8, n)
+    lens = rng.integers(min_len, max_len + 1, n)
+    pays = [rng.integers(0, 256, int(lens[i]) - 4, dtype=np.uint8) for i in range(n)]
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    sym_of = [None] * n
+    for m in range(8):
+        mod, cod = MCS8[m]
+        idx = np.nonzero(mcs == m)[0]
+        nd = ndbps(mod, cod)
+        for a in range(0, idx.size, chunk):
+            ids = idx[a:a + chunk]
+            Ls = lens[ids] - 4
+            nsyms = np.array([n_data_symbols(mod, cod, int(L)) for L in Ls])
+            S = int(nsyms.max())
+            nbits = S * nd
+            maxL = int(Ls.max())
+            byt = np.zeros((ids.size, maxL), np.uint8)
+            for r, i in enumerate(ids):
+                byt[r, :Ls[r]] = pays[i]
+            bits = np.zeros((ids.size, nbits), np.uint8)
+            bits[:, 16:16 + 8 * maxL] = np.unpackbits(byt, axis=1, bitorder="little")
+            crc = np.array([zlib.crc32(pays[i].tobytes()) for i in ids], np.uint32)
+            cpos = 16 + 8 * Ls[:, None] + np.arange(32)[None, :]
+            bits[np.arange(ids.size)[:, None], cpos] = ((crc[:, None] >> np.arange(32, dtype=np.uint32)) & 1).astype(np.uint8)
+            bits ^= _scrambler_keystream(nbits)[None]
+            u = torch.from_numpy(bits).to(device)
+            nc = NCBPS[mod]
+            coded = _encode(u, cod).reshape(ids.size, S, nc)
+            perm = torch.from_numpy(interleave_perm(mod)).to(device)
+            il = torch.empty_like(coded)
+            il[:, :, perm] = coded
+            re, im = _map(il.reshape(ids.size, S, 48, nc // 48), mod)
+            f = torch.zeros((ids.size, 1 + S, 48, 2), dtype=torch.int64, device=device)
+            f[:, 1:, :, 0] = re * UNIT[mod]
+            f[:, 1:, :, 1] = im * UNIT[mod]
+            f[:, 0, :, 0] = _signal_levels_batch(mod, cod, lens[ids], device)
+            t = to_time(f, sigma, gen)
+            for r, i in enumerate(ids):
+                sym_of[i] = t[r, :1 + nsyms[r]]
+    nsym = [int(x.shape[0]) for x in sym_of]
+    off = np.concatenate([[0], np.cumsum(nsym)[:-1]]).astype(np.int64)
+    return dict(sym=torch.cat(sym_of, 0).reshape(-1, 64, 2).contiguous(),
+                sym_off=torch.from_numpy(off).to(device), nsym=torch.tensor(nsym, dtype=torch.int32, device=device),
+                payload=pays, meta=np.stack([np.array([MCS8[int(m)][0] for m in mcs]), np.array([MCS8[int(m)][1] for m in mcs]),
+                                             lens], 1).astype(np.int32), max_nsym=int(max(nsym)))
+
+
 def make_mixed(n, min_len=64, max_len=4095, sigma=4.0, seed=0x3C5, device="cpu", unique=None):
     """BASELINE config 5: MCS uniform over the 8 rates, PSDU length (the PLCP LENGTH field,
     payload + 4 CRC bytes) uniform in [min_len, max_len].  Lengths > 2048 are header errors
