@@ -11,6 +11,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _driver():
+    if os.environ.get("ZRX_DRIVER"):                   # e.g. the sanitizer build (make asan)
+        return os.environ["ZRX_DRIVER"]
     from ziria_amd import build
     build.build()
     return build.DRIVER

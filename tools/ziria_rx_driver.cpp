@@ -83,7 +83,7 @@ bool read_samples(const Args& a, std::vector<int16_t>* v) {
   if (!read_file(a.in, &data)) return false;
   if (a.in_mode == "dbg") return parse_dbg(data, v);
   v->resize(data.size() / 2);
-  std::memcpy(v->data(), data.data(), v->size() * 2);
+  if (!v->empty()) std::memcpy(v->data(), data.data(), v->size() * 2);
   return true;
 }
 
@@ -195,7 +195,7 @@ int main(int argc, char** argv) {
     std::vector<int32_t> off(1, 0);
     std::vector<int16_t> syms;
     for (int i = 0; i < np; i++) {
-      if (first[i] < 0 || count[i] < 0 || (int64_t)(first[i] + count[i]) * 64 > nsamp) return usage();
+      if (first[i] < 0 || count[i] < 0 || ((int64_t)first[i] + count[i]) * 64 > nsamp) return usage();
       syms.insert(syms.end(), raw.begin() + 128 * (size_t)first[i], raw.begin() + 128 * (size_t)(first[i] + count[i]));
       off.push_back(off.back() + count[i]);
     }
