@@ -275,6 +275,35 @@ def test_chain_mixed_distinct_large(engine, oracle):
             assert (pay[i, :r["len"] - 4] == opay[i, :r["len"] - 4]).all(), i
 
 
+def test_viterbi_order_large_mixed_batch(oracle):
+    """k_vit_order past the old 32768-packet LDS cap: 40000 frames of mixed rates and
+    lengths (1..60 bytes, plus a few of 2048) through the device API equal the oracle."""
+    rng = np.random.default_rng(40000)
+    n = 40000
+    fl = rng.integers(1, 61, n).astype(np.int32)
+    fl[rng.choice(n, 8, replace=False)] = 2048
+    cr = rng.integers(0, 3, n).astype(np.int16)
+    K = np.array([24, 32, 36])[cr]
+    sl = ((8 * fl + 6 + K - 1) // K * 48).astype(np.int32)
+    so = (np.cumsum(sl) - sl).astype(np.int64)
+    soft = rng.integers(0, 8, int(sl.sum())).astype(np.int8)
+    oo = (np.cumsum(fl + 8) - (fl + 8)).astype(np.int64)
+    exp = oracle.viterbi_batch(soft, so, sl, fl, cr, oo, int(oo[-1] + fl[-1] + 8), nthreads=8)
+    params = torch.from_numpy(np.stack([fl, cr.astype(np.int32), sl, np.zeros(n, np.int32)], 1).copy()).cuda()
+    out = torch.zeros(int(oo[-1] + fl[-1] + 8), dtype=torch.uint8, device="cuda")
+    ob = torch.zeros(n, dtype=torch.int32, device="cuda")
+    e = RxEngine(0)
+    e.reserve(n, 1)                                      # room for the packet order
+    e.viterbi(torch.from_numpy(soft).cuda(), torch.from_numpy(so).cuda(), params, out,
+              torch.from_numpy(oo).cuda(), ob)
+    torch.cuda.synchronize()
+    e.close()
+    got = out.cpu().numpy()
+    assert (ob.cpu().numpy() == 8 * fl).all()
+    for i in range(n):
+        assert (got[oo[i]:oo[i] + fl[i]] == exp[oo[i]:oo[i] + fl[i]]).all(), i
+
+
 def test_viterbi_soft_spread_beyond_window():
     """Rows of a wave whose soft values lie more than 4 GiB apart (device API) decode one at a
     time, exactly."""
@@ -326,6 +355,25 @@ def test_chain_nsym_beyond_reservation():
     for i in (1, 3):
         assert info[i, 5] == 3 and info[i, 4] == 0 and info[i, 2] == 1504
         assert (pay[i] == 0).all()
+
+
+@pytest.mark.parametrize("sigma", [55.0, 60.0])
+def test_chain_54mbps_at_noise_edge_vs_oracle(engine, oracle, sigma):
+    """Config-3 shape where the channel noise makes a quarter to a half of the CRCs fail
+    (near-tie metrics, wrong survivors): every packet's header fields, CRC verdict and
+    payload bytes (CRC-failing ones included) equal the oracle's."""
+    b = txgen.make_batch(1024, seed=int(sigma), sigma=sigma, device="cuda")
+    engine.reserve(1024, b["max_nsym"])
+    pay, info = engine.rx(b["sym"], b["sym_off"], b["nsym"], b["max_nsym"])
+    pay, info = pay.cpu().numpy(), info.cpu().numpy()
+    opay, ores = oracle.rx_batch_time(b["sym"].cpu().numpy(), b["sym_off"].cpu().numpy(),
+                                      b["nsym"].cpu().numpy(), nthreads=8)
+    crc = np.array([r["crc_ok"] for r in ores])
+    assert 100 < (crc == 0).sum() < 1000                 # the edge is really exercised
+    for i, r in enumerate(ores):
+        assert (info[i, 2], info[i, 3], info[i, 4]) == (r["len"], r["err"], r["crc_ok"]), i
+        if not r["err"]:
+            assert (pay[i, :r["len"] - 4] == opay[i, :r["len"] - 4]).all(), i
 
 
 def test_chain_large_batch_properties(engine):

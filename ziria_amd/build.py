@@ -38,18 +38,28 @@ DRIVER = os.path.join(LIBDIR, "ziria_rx_driver")
 DRIVER_SRC = os.path.join(HERE, "..", "tools", "ziria_rx_driver.cpp")
 
 
-def build_driver(verbose=False):
-    """The batching driver (tools/ziria_rx_driver.cpp), a host program linked against the
-    library (rpath $ORIGIN, next to it in ziria_amd/_lib)."""
-    if os.path.exists(DRIVER) and os.path.getmtime(DRIVER) >= max(os.path.getmtime(DRIVER_SRC), os.path.getmtime(LIB)):
-        return DRIVER
-    cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-o", DRIVER + ".tmp", DRIVER_SRC, "-L" + LIBDIR, "-lziria_rx",
+PERCALL = os.path.join(LIBDIR, "percall_bench")
+PERCALL_SRC = os.path.join(HERE, "..", "tools", "percall_bench.cpp")
+
+
+def _host_tool(exe, src, verbose):
+    if os.path.exists(exe) and os.path.getmtime(exe) >= max(os.path.getmtime(src), os.path.getmtime(LIB)):
+        return exe
+    cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-o", exe + ".tmp", src, "-L" + LIBDIR, "-lziria_rx",
            "-Wl,-rpath,$ORIGIN"]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)
-    os.replace(DRIVER + ".tmp", DRIVER)
-    return DRIVER
+    os.replace(exe + ".tmp", exe)
+    return exe
+
+
+def build_driver(verbose=False):
+    """The host programs linked against the library (rpath $ORIGIN, next to it in
+    ziria_amd/_lib): the batching driver (tools/ziria_rx_driver.cpp) and the per-call
+    latency bench (tools/percall_bench.cpp)."""
+    _host_tool(PERCALL, PERCALL_SRC, verbose)
+    return _host_tool(DRIVER, DRIVER_SRC, verbose)
 
 
 def build(force=False, verbose=False):

@@ -50,6 +50,8 @@ struct zrx_ctx {
   int32_t* vparams = nullptr;     // 4 int32 per packet
   uint8_t* soft = nullptr;        // soft_stride B per packet
   int64_t* soft_off = nullptr;    // per packet, packed by soft_len (k_soft_scan)
+  int32_t* dsym = nullptr;        // data-symbol prefix per packet, npkts + 1 (k_soft_scan)
+  int32_t* wave_p0 = nullptr;     // first packet of each k_data_fft wave (k_soft_scan)
   uint8_t* dec = nullptr;         // kDecStride B per packet
   int64_t* dec_off = nullptr;     // p * kDecStride
   int32_t* dec_bits = nullptr;
@@ -96,11 +98,11 @@ static int check_device(int device) {
 }
 
 static void free_ws(zrx_ctx* c) {
-  for (void* p : {(void*)c->sig_soft, (void*)c->vparams, (void*)c->soft, (void*)c->soft_off, (void*)c->dec,
-                  (void*)c->dec_off, (void*)c->dec_bits, (void*)c->order})
+  for (void* p : {(void*)c->sig_soft, (void*)c->vparams, (void*)c->soft, (void*)c->soft_off, (void*)c->dsym,
+                  (void*)c->wave_p0, (void*)c->dec, (void*)c->dec_off, (void*)c->dec_bits, (void*)c->order})
     (void)hipFree(p);
   c->sig_soft = nullptr; c->vparams = nullptr; c->soft = nullptr; c->soft_off = nullptr;
-  c->dec = nullptr; c->dec_off = nullptr; c->dec_bits = nullptr; c->order = nullptr;
+  c->dsym = nullptr; c->wave_p0 = nullptr; c->dec = nullptr; c->dec_off = nullptr; c->dec_bits = nullptr; c->order = nullptr;
   c->cap_pkts = c->cap_nsym = 0;
 }
 
@@ -287,7 +289,7 @@ static bool order_fits(const zrx_ctx* c, int npkts) {
 #ifdef ZRX_EXPERIMENTS
   if (c->vit_impl != 3) return false;
 #endif
-  return c->use_order && c->order && npkts <= c->cap_pkts && npkts <= kOrderMax;
+  return c->use_order && c->order && npkts <= c->cap_pkts;
 }
 
 // Every launch function starts here: a launch on a different stream than the previous one
@@ -441,6 +443,8 @@ int zrx_reserve(zrx_ctx* c, int npkts, int max_nsym) {
   ZRX_CHECK(hipMalloc(&c->vparams, (size_t)np * 16 + 16));
   ZRX_CHECK(hipMalloc(&c->soft, (size_t)np * stride + 256));
   ZRX_CHECK(hipMalloc(&c->soft_off, (size_t)np * 8 + 8));
+  ZRX_CHECK(hipMalloc(&c->dsym, (size_t)np * 4 + 8));
+  ZRX_CHECK(hipMalloc(&c->wave_p0, ((size_t)np * std::max(ns - 1, 1) / 64 + 2) * 4));
   ZRX_CHECK(hipMalloc(&c->dec, (size_t)np * kDecStride + 256));
   ZRX_CHECK(hipMalloc(&c->dec_off, (size_t)np * 8 + 8));
   ZRX_CHECK(hipMalloc(&c->dec_bits, (size_t)np * 4 + 4));
@@ -513,7 +517,7 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
                                                            (uint4*)c->sig_soft, chan, T);
   if (ev) ZRX_CHECK(hipEventRecord(ev[1], s));
   k_signal_vit<<<blocks(npkts, 4), 256, 0, s>>>(c->sig_soft, d_nsym, npkts, c->cap_nsym, c->vparams, d_info);
-  k_soft_scan<<<1, 1024, 0, s>>>(c->vparams, npkts, c->soft_off);   // packed soft slots
+  k_soft_scan<<<1, 1024, 0, s>>>(c->vparams, npkts, c->soft_off, c->dsym, c->wave_p0);
   if (ev) ZRX_CHECK(hipEventRecord(ev[2], s));
   // the Viterbi packet order needs only the headers: one block on the side stream, hidden
   // behind k_data_fft (a 1-block kernel costs ~20 us in line)
@@ -529,12 +533,16 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
     k_vit_order<<<1, 1024, 0, c->side>>>(c->vparams, npkts, c->order);
     ZRX_CHECK(hipEventRecord(c->join, c->side));
   }
-  if (chan)
-    k_data_fft<true><<<blocks(npkts, 4), 256, 0, s>>>((const uint4*)d_sym, d_sym_off, c->vparams, npkts,
-                                                      (uint4*)c->soft, c->soft_off, chan, T);
-  else
-    k_data_fft<false><<<blocks(npkts, 4), 256, 0, s>>>((const uint4*)d_sym, d_sym_off, c->vparams, npkts,
-                                                       (uint4*)c->soft, c->soft_off, chan, T);
+  // k_data_fft: waves over the batch's data symbols, at most npkts x (max_nsym - 1) of them
+  const int fft_blocks = (int)std::min<int64_t>(((int64_t)npkts * (max_nsym - 1) + 255) / 256, kDataFftBlocks);
+  if (fft_blocks > 0) {
+    if (chan)
+      k_data_fft<true><<<fft_blocks, 256, 0, s>>>((const uint4*)d_sym, d_sym_off, c->vparams, npkts, (uint4*)c->soft,
+                                                   c->soft_off, c->dsym, c->wave_p0, chan, T);
+    else
+      k_data_fft<false><<<fft_blocks, 256, 0, s>>>((const uint4*)d_sym, d_sym_off, c->vparams, npkts, (uint4*)c->soft,
+                                                    c->soft_off, c->dsym, c->wave_p0, chan, T);
+  }
   if (ev) ZRX_CHECK(hipEventRecord(ev[3], s));
   if (side_order) ZRX_CHECK(hipStreamWaitEvent(s, c->join, 0));
   launch_viterbi(c, c->soft, c->soft_off, c->vparams, npkts, c->dec, c->dec_off, c->dec_bits, side_order);

@@ -5,7 +5,7 @@
 //                    DeinterleaveBPSK (DecodePLCP.blk:30-37)
 //   k_signal_vit     one wave per packet: Viterbi_sig11 (viterbicore.hpp:272-315) +
 //                    parsePLCPHeader (parsePLCPHeader.blk:119-213)
-//   k_data_fft       one wave per packet, lane = data symbol: FFT -> GetData -> DemapLimit ->
+//   k_data_fft       lane = data symbol, flat over the batch: FFT -> GetData -> DemapLimit ->
 //                    Demap{mod} -> Deinterleave{mod} (Decode.blk:45-60); with EQ, ChannelEqualization
 //                    + PilotTrack after the FFT (receiver.blk:66-71), also in k_signal_fft
 //   k_ofdm_eq        FFT -> ChannelEqualization -> PilotTrack, full 64-bin output
@@ -209,71 +209,94 @@ __global__ __launch_bounds__(256) void k_signal_vit(const uint32_t* __restrict__
   }
 }
 
-// Soft-value slots of the rx chain, packed by what each packet's header asks for:
-// off[p] = sum over q < p of soft_len(q) rounded up to 256 B (vparams[4q+2], k_signal_vit).
-// One 1024-thread block: a contiguous run of packets per thread, then a block scan.  Packed
-// slots keep a batch's soft values within the Viterbi's 4 GiB read window (a mixed batch
-// sized for its longest packet at 64-QAM would not be).
+// Soft-value slots and data-symbol numbering of the rx chain, from what each packet's header
+// asks for (vparams[4q+2] = soft_len, k_signal_vit):
+//   off[p]       = sum over q < p of soft_len(q) rounded up to 256 B (packed soft slots: a
+//                  batch's soft values stay within the Viterbi's 4 GiB read window, which a
+//                  mixed batch sized for its longest packet at 64-QAM would not);
+//   dsym[p]      = sum over q < p of the data symbols of q; dsym[npkts] = all of them;
+//   wave_p0[w]   = the packet holding batch data symbol 64w (k_data_fft's waves).
+// One 1024-thread block: a contiguous run of packets per thread, then one block scan of
+// both sums packed in a 64-bit word (256-B units above, symbols below; each < 2^32).
 __global__ __launch_bounds__(1024) void k_soft_scan(const int32_t* __restrict__ vparams, int npkts,
-                                                    int64_t* __restrict__ off) {
-  __shared__ int64_t wsum[16];
+                                                    int64_t* __restrict__ off, int32_t* __restrict__ dsym,
+                                                    int32_t* __restrict__ wave_p0) {
+  __shared__ uint64_t wsum[16];
   const int t = threadIdx.x;
   const int per = (npkts + 1023) / 1024;
   const int lo = min(t * per, npkts), hi = min(lo + per, npkts);
-  int64_t mine = 0;
-  for (int p = lo; p < hi; p++) mine += (int64_t)((vparams[4 * (int64_t)p + 2] + 255) & ~255);
-  int64_t inc = mine;                                  // inclusive scan inside the wave
+  auto item = [vparams](int p) {
+    const int32_t* vp = vparams + 4 * (int64_t)p;
+    const uint32_t n = (uint32_t)max(vp[2], 0);
+    return ((uint64_t)((n + 255u) >> 8) << 32) | (uint64_t)(n / (uint32_t)ncbps_of(vp[3]));
+  };
+  uint64_t mine = 0;
+  for (int p = lo; p < hi; p++) mine += item(p);
+  uint64_t inc = mine;                                 // inclusive scan inside the wave
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
-    const int64_t u = __shfl_up(inc, o);
+    const uint64_t u = __shfl_up(inc, o);
     if ((t & 63) >= o) inc += u;
   }
   if ((t & 63) == 63) wsum[t >> 6] = inc;
   __syncthreads();
-  int64_t base = inc - mine;
+  uint64_t base = inc - mine;
   for (int w = 0; w < (t >> 6); w++) base += wsum[w];
   for (int p = lo; p < hi; p++) {
-    off[p] = base;
-    base += (int64_t)((vparams[4 * (int64_t)p + 2] + 255) & ~255);
+    const uint64_t it = item(p);
+    const uint32_t s0 = (uint32_t)base, s1 = s0 + (uint32_t)it;
+    off[p] = (int64_t)(base >> 32) << 8;
+    dsym[p] = (int32_t)s0;
+    for (uint32_t w = (s0 + 63u) >> 6; 64u * w < s1; w++) wave_p0[w] = p;
+    base += it;
   }
+  if (t == 1023) dsym[npkts] = (int32_t)(uint32_t)base;   // the whole batch's data symbols
 }
 
 // ------------------------------------------------------------------ data symbols -> soft
+constexpr int kDataFftBlocks = 2048;  // k_data_fft grid cap: 8192 waves, 32 per CU, looping
+
 template <int MOD, bool EQ>
-__device__ __forceinline__ void data_fft_packet(const uint4* __restrict__ sym0, int need, int lane,
-                                                const uint32_t* lut, uint4* __restrict__ dst0,
-                                                const uint32_t* __restrict__ cp, const EqTabs& T) {
-  constexpr int NC = ModInfo<MOD>::ncbps;
-  for (int k = lane; k < need; k += 64) {
-    s2 x[64];
-    load_symbol(sym0 + (int64_t)k * 16, x);
-    fft64_inplace(x);
-    if constexpr (EQ) equalize_data_bins(x, [cp](int b) { return as_s2(cp[b]); }, k + 1, T);
-    uint4* dst = dst0 + (int64_t)k * (NC / 16);
-    demap_deinterleave_st<MOD>(x, lut, [dst](int q, uint4 v) { dst[q] = v; });
-  }
+__device__ __forceinline__ void data_fft_symbol(const uint4* __restrict__ src, int k, const uint32_t* lut,
+                                                uint4* __restrict__ dst, const uint32_t* __restrict__ cp,
+                                                const EqTabs& T) {
+  s2 x[64];
+  load_symbol(src, x);
+  fft64_inplace(x);
+  if constexpr (EQ) equalize_data_bins(x, [cp](int b) { return as_s2(cp[b]); }, k + 1, T);
+  demap_deinterleave_st<MOD>(x, lut, [dst](int q, uint4 v) { dst[q] = v; });
 }
+// Flat over the batch's data symbols (k_soft_scan numbers them): wave w takes symbols
+// 64w .. 64w+63, lane = symbol, whatever packets they belong to, so a long packet spreads
+// over many waves and consecutive lanes write consecutive soft rows.  Waves loop over w with
+// the grid's stride (the host sizes the grid from the call's max_nsym, an upper bound).
 template <bool EQ>
 __global__ __launch_bounds__(256) void k_data_fft(const uint4* __restrict__ sym, const int64_t* __restrict__ sym_off,
                                                   const int32_t* __restrict__ vparams, int npkts,
                                                   uint4* __restrict__ soft, const int64_t* __restrict__ soft_off,
+                                                  const int32_t* __restrict__ dsym, const int32_t* __restrict__ wave_p0,
                                                   const uint32_t* __restrict__ chan, EqTabs T) {
   __shared__ uint32_t lut[256];
   stage_lut(lut);
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int p = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wv);   // one packet per wave
-  if (p >= npkts) return;
-  const uint32_t* cp = EQ ? chan + (int64_t)p * 64 : nullptr;        // wave-uniform: scalar loads
-  const int32_t* vp = vparams + 4 * (int64_t)p;
-  const int soft_len = vp[2], mod = vp[3];
-  if (soft_len <= 0) return;
-  const uint4* s0 = sym + (sym_off[p] + 1) * 16;
-  uint4* d0 = soft + soft_off[p] / 16;
-  switch (mod) {
-    case 0: data_fft_packet<0, EQ>(s0, soft_len / 48, lane, lut, d0, cp, T); break;
-    case 1: data_fft_packet<1, EQ>(s0, soft_len / 96, lane, lut, d0, cp, T); break;
-    case 2: data_fft_packet<2, EQ>(s0, soft_len / 192, lane, lut, d0, cp, T); break;
-    default: data_fft_packet<3, EQ>(s0, soft_len / 288, lane, lut, d0, cp, T); break;
+  const int lane = threadIdx.x & 63;
+  const int total = dsym[npkts];
+  const int nw = (total + 63) >> 6;
+  for (int w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); w < nw; w += gridDim.x * 4) {
+    const int g = w * 64 + lane;
+    if (g >= total) continue;
+    int p = wave_p0[w];
+    while (dsym[p + 1] <= g) p++;                    // packets of fewer than 64 symbols
+    const int k = g - dsym[p];
+    const int mod = vparams[4 * (int64_t)p + 3];
+    const uint4* src = sym + (sym_off[p] + 1 + k) * 16;
+    uint4* dst = soft + soft_off[p] / 16;
+    const uint32_t* cp = EQ ? chan + (int64_t)p * 64 : nullptr;
+    switch (mod) {
+      case 0: data_fft_symbol<0, EQ>(src, k, lut, dst + k * 3, cp, T); break;
+      case 1: data_fft_symbol<1, EQ>(src, k, lut, dst + k * 6, cp, T); break;
+      case 2: data_fft_symbol<2, EQ>(src, k, lut, dst + k * 12, cp, T); break;
+      default: data_fft_symbol<3, EQ>(src, k, lut, dst + k * 18, cp, T); break;
+    }
   }
 }
 

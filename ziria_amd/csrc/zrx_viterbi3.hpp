@@ -218,7 +218,16 @@ __device__ __forceinline__ void column5(uint32_t& M0, uint32_t& M1, uint32_t P, 
     else if constexpr (PH == 4) BX1 = BX0 ^ mbits;
     else BX1 = __builtin_amdgcn_perm((mk & 0xFFu) * 0x01010101u, P, K.sel[PH][1]);
   }
-  const uint32_t BY0 = C - BX0, BY1 = C - BX1;
+  // Keep C - BX a value of its own: reassociated as (partner T - BX) + C it would put two
+  // adds after the AND on the column-to-column dependency chain instead of one (a wave
+  // alone on its SIMD waits out that chain every column).
+  uint32_t BY0 = C - BX0;
+  asm("" : "+v"(BY0));
+  uint32_t BY1 = BY0;
+  if constexpr (PH != 2) {
+    BY1 = C - BX1;
+    asm("" : "+v"(BY1));
+  }
   const uint32_t X0 = T0 + BX0, X1 = T1 + BX1;
   uint32_t Z0, Z1;
   if constexpr (PH <= 3) {
@@ -765,9 +774,13 @@ __global__ __launch_bounds__(256, 4) void k_viterbi3(const uint8_t* __restrict__
 // trellis length, longest first, so the four rows of a wave share one rate and similar
 // lengths.  One 1024-thread block; counting sort over (rate, 24-column bodies) keys, with
 // runs of equal keys in a thread's contiguous slice counted by one LDS atomic (a uniform
-// batch costs 1024 atomics, not one per packet).
-constexpr int kOrderLen = 512;                         // length buckets of 24 columns
+// batch costs 1024 atomics, not one per packet).  Keys are recomputed from vparams in the
+// scatter pass (no per-packet LDS), so any batch size is ordered; 1024 length buckets cover
+// 24576 columns, i.e. every 802.11a frame (at most 8 x 2050 + 6 = 16406 columns); longer
+// device-API frames share the last bucket.
+constexpr int kOrderLen = 1024;                        // length buckets of 24 columns
 constexpr int kOrderKeys = 3 * kOrderLen + 1;          // + one bucket for packets with no work
+constexpr int kOrderPerThread = (kOrderKeys + 1023) / 1024;
 __device__ __forceinline__ uint32_t order_key(const int32_t* __restrict__ vparams, int p) {
   const int32_t* vp = vparams + 4 * (int64_t)p;
   const int cr = vp[1], n = vp[2];
@@ -776,30 +789,28 @@ __device__ __forceinline__ uint32_t order_key(const int32_t* __restrict__ vparam
   const uint32_t bodies = min((cols + 23u) / 24u, (uint32_t)kOrderLen - 1u);
   return (uint32_t)cr * kOrderLen + (kOrderLen - 1u - bodies);
 }
-constexpr int kOrderMax = 32768;                       // batch size the LDS key stage holds
 __global__ __launch_bounds__(1024) void k_vit_order(const int32_t* __restrict__ vparams, int npkts,
                                                     int32_t* __restrict__ order) {
-  __shared__ uint32_t hist[kOrderKeys];
-  __shared__ uint16_t keys[kOrderMax];
-  for (int i = threadIdx.x; i < kOrderKeys; i += blockDim.x) hist[i] = 0;
-  for (int p = threadIdx.x; p < npkts; p += blockDim.x) keys[p] = (uint16_t)order_key(vparams, p);  // coalesced
+  __shared__ uint32_t hist[kOrderPerThread * 1024];
+  for (int i = threadIdx.x; i < kOrderPerThread * 1024; i += blockDim.x) hist[i] = 0;
   __syncthreads();
   const int per = (npkts + (int)blockDim.x - 1) / (int)blockDim.x;
   const int lo = min((int)threadIdx.x * per, npkts), hi = min(lo + per, npkts);
   uint32_t prev = 0xFFFFFFFFu, run = 0;
   for (int p = lo; p < hi; p++) {
-    const uint32_t k = keys[p];
+    const uint32_t k = order_key(vparams, p);
     if (k == prev) { run++; continue; }
     if (run) atomicAdd(&hist[prev], run);
     prev = k; run = 1;
   }
   if (run) atomicAdd(&hist[prev], run);
   __syncthreads();
-  {                                                    // exclusive scan: 2 buckets per thread
+  {                                                    // exclusive scan: kOrderPerThread buckets per thread
     __shared__ uint32_t wsum[16];
-    const int t = threadIdx.x, i0 = 2 * t, i1 = 2 * t + 1;
-    const uint32_t v0 = i0 < kOrderKeys ? hist[i0] : 0u, v1 = i1 < kOrderKeys ? hist[i1] : 0u;
-    const uint32_t mine = v0 + v1;
+    const int t = threadIdx.x;
+    uint32_t v[kOrderPerThread], mine = 0;
+#pragma unroll
+    for (int j = 0; j < kOrderPerThread; j++) { v[j] = hist[kOrderPerThread * t + j]; mine += v[j]; }
     uint32_t inc = mine;                               // inclusive scan inside the wave
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -808,18 +819,17 @@ __global__ __launch_bounds__(1024) void k_vit_order(const int32_t* __restrict__ 
     }
     if ((t & 63) == 63) wsum[t >> 6] = inc;
     __syncthreads();
-    uint32_t wbase = 0;
-    for (int w = 0; w < (t >> 6); w++) wbase += wsum[w];
-    const uint32_t ex = wbase + inc - mine;
+    uint32_t ex = inc - mine;
+    for (int w = 0; w < (t >> 6); w++) ex += wsum[w];
     __syncthreads();
-    if (i0 < kOrderKeys) hist[i0] = ex;
-    if (i1 < kOrderKeys) hist[i1] = ex + v0;
+#pragma unroll
+    for (int j = 0; j < kOrderPerThread; j++) { hist[kOrderPerThread * t + j] = ex; ex += v[j]; }
   }
   __syncthreads();
   prev = 0xFFFFFFFFu; run = 0;
   int start = lo;
   for (int p = lo; p <= hi; p++) {
-    const uint32_t k = p < hi ? (uint32_t)keys[p] : 0xFFFFFFFEu;
+    const uint32_t k = p < hi ? order_key(vparams, p) : 0xFFFFFFFEu;
     if (k == prev) { run++; continue; }
     if (run) {
       const uint32_t base = atomicAdd(&hist[prev], run);
