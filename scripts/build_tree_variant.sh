@@ -1,0 +1,22 @@
+#!/bin/bash
+# Builds the working tree's engine with one text substitution applied (A/B of an uncommitted
+# change): scripts/build_tree_variant.sh NAME FILE OLD_TEXT_FILE NEW_TEXT_FILE
+# -> ziria_amd/_lib/libziria_rx.NAME.so (ZRX_EXPERIMENTS build, as build_variant.sh).
+set -euo pipefail
+NAME=$1; FILE=$2; OLD=$3; NEW=$4
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+TMP=$(mktemp -d)
+trap 'rm -rf "$TMP"' EXIT
+mkdir -p "$TMP/ziria_amd" "$TMP/include"
+cp -r "$ROOT/ziria_amd/csrc" "$TMP/ziria_amd/"
+cp "$ROOT/include/ziria_rx.h" "$TMP/include/"
+python3 - "$TMP/ziria_amd/csrc/$FILE" "$OLD" "$NEW" <<'PY'
+import sys
+p, o, n = sys.argv[1:]
+s = open(p).read(); old = open(o).read(); new = open(n).read()
+assert old in s, "old text not found"
+open(p, "w").write(s.replace(old, new))
+PY
+cd "$TMP/ziria_amd/csrc"
+hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DZRX_EXPERIMENTS -o "$ROOT/ziria_amd/_lib/libziria_rx.$NAME.so" zrx_api.hip
+echo "$ROOT/ziria_amd/_lib/libziria_rx.$NAME.so"

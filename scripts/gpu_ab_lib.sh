@@ -7,11 +7,11 @@ mkdir -p gpurun_out
 for r in $(seq ${ROUNDS:-2}); do
   for v in ${VARIANTS:-cur}; do
     if [ "$v" = cur ]; then unset ZRX_LIB_VARIANT; else export ZRX_LIB_VARIANT=$v; fi
-    timeout -k 10 200 python bench.py --steps ${STEPS:-5} --warmup 2 --no-cpu ${BENCH_ARGS:-} > gpurun_out/ab_${v}_$r.log 2>&1; rc=$?
-    [ $rc -eq 0 ] || { echo "$v rc=$rc"; tail -5 gpurun_out/ab_${v}_$r.log; exit $rc; }
+    timeout -k 10 200 python bench.py --steps ${STEPS:-5} --warmup 2 --no-cpu ${BENCH_ARGS:-} > gpurun_out/ab${AB_TAG:-}_${v}_$r.log 2>&1; rc=$?
+    [ $rc -eq 0 ] || { echo "$v rc=$rc"; tail -5 gpurun_out/ab${AB_TAG:-}_${v}_$r.log; exit $rc; }
     python -c "
 import json
-for l in open('gpurun_out/ab_${v}_$r.log'):
-    if l.startswith('{'): d=json.loads(l); print('$v', d.get('stage_ms', {}).get('data_viterbi'), d['ms_per_step'], d['value'], d.get('bit_exact_check', d.get('frames_equal_sent')))"
+for l in open('gpurun_out/ab${AB_TAG:-}_${v}_$r.log'):
+    if l.startswith('{'): d=json.loads(l); sm=d.get('stage_ms', {}); print('$v', sm.get('data_viterbi'), sm.get('data_fft_demap'), sm.get('signal_viterbi'), d['ms_per_step'], d['value'], d.get('bit_exact_check', {}).get('payload_match') if 'bit_exact_check' in d else d.get('frames_equal_sent'))"
   done
 done

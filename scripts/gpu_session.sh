@@ -13,13 +13,16 @@ echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
 step ab
 VARIANTS="${VARIANTS:-cur}" ROUNDS=${ROUNDS:-2} ./scripts/gpu_ab_lib.sh || exit 1
 step ab-config2
-VARIANTS="${VARIANTS2:-${VARIANTS:-cur}}" ROUNDS=${ROUNDS:-2} BENCH_ARGS="--config 2" ./scripts/gpu_ab_lib.sh || exit 1
+AB_TAG=c2 VARIANTS="${VARIANTS2:-${VARIANTS:-cur}}" ROUNDS=${ROUNDS:-2} BENCH_ARGS="--config 2" ./scripts/gpu_ab_lib.sh || exit 1
 step config5
 timeout -k 10 300 python bench.py --config 5 --steps 10 > gpurun_out/bench_c5.log 2>&1 || { tail -5 gpurun_out/bench_c5.log; exit 1; }
 tail -1 gpurun_out/bench_c5.log | cut -c1-900
 step config5-rocprof
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5 -o run -- python bench.py --config 5 --steps 5 --warmup 2 --no-cpu > gpurun_out/prof_c5.log 2>&1 || { tail -5 gpurun_out/prof_c5.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c5 -o run -- python bench.py --config 5 --steps 5 --warmup 2 --no-cpu > gpurun_out/prof_c5.log 2>&1 || { tail -5 gpurun_out/prof_c5.log; exit 1; }
 find gpurun_out/prof_c5 -name "*kernel_stats.csv" | head -1 | xargs -r head -12 | cut -d, -f1-8
+step config3-rocprof
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3 -o run -- python bench.py --steps 10 --warmup 2 --no-cpu > gpurun_out/prof_c3.log 2>&1 || { tail -5 gpurun_out/prof_c3.log; exit 1; }
+find gpurun_out/prof_c3 -name "*kernel_stats.csv" | head -1 | xargs -r head -12 | cut -d, -f1-8
 step percall
 timeout -k 10 120 ziria_amd/_lib/percall_bench 10 1500 > gpurun_out/percall.json 2>&1 || { cat gpurun_out/percall.json; exit 1; }
 cat gpurun_out/percall.json

@@ -49,17 +49,14 @@ struct zrx_ctx {
   uint32_t* sig_soft = nullptr;   // 48 B per packet
   int32_t* vparams = nullptr;     // 4 int32 per packet
   uint8_t* soft = nullptr;        // soft_stride B per packet
-  int64_t* soft_off = nullptr;    // per packet, packed by soft_len (k_soft_scan)
-  int32_t* dsym = nullptr;        // data-symbol prefix per packet, npkts + 1 (k_soft_scan)
-  int32_t* wave_p0 = nullptr;     // first packet of each k_data_fft wave (k_soft_scan)
+  int64_t* soft_off = nullptr;    // per packet, packed by soft_len (k_pkt_plan)
+  int32_t* dsym = nullptr;        // data-symbol prefix per packet, npkts + 1 (k_pkt_plan)
+  int32_t* wave_p0 = nullptr;     // first packet of each k_data_fft wave (k_pkt_plan)
   uint8_t* dec = nullptr;         // kDecStride B per packet
   int64_t* dec_off = nullptr;     // p * kDecStride
   int32_t* dec_bits = nullptr;
   int32_t* order = nullptr;       // Viterbi packet order (k_vit_order)
   bool use_order = true;          // ZRX_ORDER=0 (experiment builds) turns the ordering off
-  // rx chain: k_vit_order runs on a side stream beside k_data_fft (fork/join by events)
-  hipStream_t side = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
   // The workspace is shared by every launch of this context: a launch on a different stream
   // than the previous one first waits for the previous launch's work (ws_free).
   hipEvent_t ws_free = nullptr;
@@ -306,7 +303,7 @@ static int ws_release(zrx_ctx* c) {
   return ZRX_OK;
 }
 
-// order_ready: the caller already ran k_vit_order into c->order (rx chain, side stream)
+// order_ready: the caller already wrote the packet order into c->order (rx chain: k_pkt_plan)
 static void launch_viterbi(zrx_ctx* c, const uint8_t* soft, const int64_t* soft_off, const int32_t* params,
                            int npkts, uint8_t* out, const int64_t* out_off, int32_t* out_bits,
                            bool order_ready = false) {
@@ -385,12 +382,6 @@ int zrx_destroy(zrx_ctx* c) {
     (void)hipFree(p);
   (void)hipFree(c->vstream);
   (void)hipFree(c->small);
-  if (c->side) {
-    (void)hipStreamSynchronize(c->side);
-    (void)hipStreamDestroy(c->side);
-    (void)hipEventDestroy(c->fork);
-    (void)hipEventDestroy(c->join);
-  }
   for (auto& set : c->evsets)
     for (auto& e : set) (void)hipEventDestroy(e);
   if (c->ws_free) (void)hipEventDestroy(c->ws_free);
@@ -517,22 +508,9 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
                                                            (uint4*)c->sig_soft, chan, T);
   if (ev) ZRX_CHECK(hipEventRecord(ev[1], s));
   k_signal_vit<<<blocks(npkts, 4), 256, 0, s>>>(c->sig_soft, d_nsym, npkts, c->cap_nsym, c->vparams, d_info);
-  k_soft_scan<<<1, 1024, 0, s>>>(c->vparams, npkts, c->soft_off, c->dsym, c->wave_p0);
+  const bool ordered = order_fits(c, npkts);
+  k_pkt_plan<<<1, 1024, 0, s>>>(c->vparams, npkts, c->soft_off, c->dsym, c->wave_p0, ordered ? c->order : nullptr);
   if (ev) ZRX_CHECK(hipEventRecord(ev[2], s));
-  // the Viterbi packet order needs only the headers: one block on the side stream, hidden
-  // behind k_data_fft (a 1-block kernel costs ~20 us in line)
-  const bool side_order = order_fits(c, npkts);
-  if (side_order) {
-    if (!c->side) {
-      ZRX_CHECK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
-      ZRX_CHECK(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
-      ZRX_CHECK(hipEventCreateWithFlags(&c->join, hipEventDisableTiming));
-    }
-    ZRX_CHECK(hipEventRecord(c->fork, s));
-    ZRX_CHECK(hipStreamWaitEvent(c->side, c->fork, 0));
-    k_vit_order<<<1, 1024, 0, c->side>>>(c->vparams, npkts, c->order);
-    ZRX_CHECK(hipEventRecord(c->join, c->side));
-  }
   // k_data_fft: waves over the batch's data symbols, at most npkts x (max_nsym - 1) of them
   const int fft_blocks = (int)std::min<int64_t>(((int64_t)npkts * (max_nsym - 1) + 255) / 256, kDataFftBlocks);
   if (fft_blocks > 0) {
@@ -544,8 +522,7 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
                                                     c->soft_off, c->dsym, c->wave_p0, chan, T);
   }
   if (ev) ZRX_CHECK(hipEventRecord(ev[3], s));
-  if (side_order) ZRX_CHECK(hipStreamWaitEvent(s, c->join, 0));
-  launch_viterbi(c, c->soft, c->soft_off, c->vparams, npkts, c->dec, c->dec_off, c->dec_bits, side_order);
+  launch_viterbi(c, c->soft, c->soft_off, c->vparams, npkts, c->dec, c->dec_off, c->dec_bits, ordered);
   if (ev) ZRX_CHECK(hipEventRecord(ev[4], s));
   k_descramble_crc<<<c->crc_blocks > 0 ? std::min(blocks(npkts, kCrcWaves), c->crc_blocks) : blocks(npkts, kCrcWaves),
                      64 * kCrcWaves, 0, s>>>(c->dec, c->dec_bits, d_info, d_payload, npkts);

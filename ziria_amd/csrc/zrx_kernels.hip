@@ -209,51 +209,121 @@ __global__ __launch_bounds__(256) void k_signal_vit(const uint32_t* __restrict__
   }
 }
 
-// Soft-value slots and data-symbol numbering of the rx chain, from what each packet's header
-// asks for (vparams[4q+2] = soft_len, k_signal_vit):
+// The rx chain's per-batch plan, from what each packet's header asks for (vparams,
+// k_signal_vit), in one kernel right after it:
 //   off[p]       = sum over q < p of soft_len(q) rounded up to 256 B (packed soft slots: a
 //                  batch's soft values stay within the Viterbi's 4 GiB read window, which a
 //                  mixed batch sized for its longest packet at 64-QAM would not);
 //   dsym[p]      = sum over q < p of the data symbols of q; dsym[npkts] = all of them;
-//   wave_p0[w]   = the packet holding batch data symbol 64w (k_data_fft's waves).
-// One 1024-thread block: a contiguous run of packets per thread, then one block scan of
-// both sums packed in a 64-bit word (256-B units above, symbols below; each < 2^32).
-__global__ __launch_bounds__(1024) void k_soft_scan(const int32_t* __restrict__ vparams, int npkts,
-                                                    int64_t* __restrict__ off, int32_t* __restrict__ dsym,
-                                                    int32_t* __restrict__ wave_p0) {
-  __shared__ uint64_t wsum[16];
-  const int t = threadIdx.x;
-  const int per = (npkts + 1023) / 1024;
-  const int lo = min(t * per, npkts), hi = min(lo + per, npkts);
-  auto item = [vparams](int p) {
-    const int32_t* vp = vparams + 4 * (int64_t)p;
-    const uint32_t n = (uint32_t)max(vp[2], 0);
-    return ((uint64_t)((n + 255u) >> 8) << 32) | (uint64_t)(n / (uint32_t)ncbps_of(vp[3]));
-  };
-  uint64_t mine = 0;
-  for (int p = lo; p < hi; p++) mine += item(p);
-  uint64_t inc = mine;                                 // inclusive scan inside the wave
+//   wave_p0[w]   = the packet holding batch data symbol 64w (k_data_fft's waves);
+//   order        = k_viterbi3's packet order (k_vit_order's counting sort, same keys), when
+//                  not null.
+// One 1024-thread block, rounds of 16 x 1024 packets: every thread loads its 16 packets'
+// parameters (p = round base + 1024 i + thread: coalesced, all loads in flight together),
+// 16 independent DPP wave scans of the two 32-bit sums (256-B units, symbols), one table of
+// 256 (chunk, wave) offsets scanned by wave 0, every thread's 16 offsets from it; the order
+// keys are counted in the same pass and scattered in a second one.  (As separate kernels,
+// the order ran on a side stream and its join, with the fork, cost ~45 us per step.)
+constexpr int kScanPer = 16;
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);   // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);   // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);   // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);   // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return x;
+}
+__global__ __launch_bounds__(1024) void k_pkt_plan(const int32_t* __restrict__ vparams, int npkts,
+                                                   int64_t* __restrict__ off, int32_t* __restrict__ dsym,
+                                                   int32_t* __restrict__ wave_p0, int32_t* __restrict__ order) {
+  __shared__ uint2 wtab[kScanPer * 16];                // (chunk i, wave w) totals, then offsets
+  __shared__ uint2 round_total;
+  __shared__ uint32_t hist[kOrderPerThread * 1024];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (order) {
+    for (int i = t; i < kOrderPerThread * 1024; i += 1024) hist[i] = 0;
+    __syncthreads();
+  }
+  uint64_t carry_u = 0;                                // 256-B units before this round
+  uint32_t carry_s = 0;                                // symbols before this round
+  uint32_t key[kScanPer];                              // the last round's keys (the only round up to 16384 packets)
+  for (int base = 0; base < npkts; base += 1024 * kScanPer) {
+    uint32_t vu[kScanPer], vs[kScanPer], iu[kScanPer], is[kScanPer];
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint64_t u = __shfl_up(inc, o);
-    if ((t & 63) >= o) inc += u;
+    for (int i = 0; i < kScanPer; i++) {
+      const int p = base + 1024 * i + t;
+      vu[i] = vs[i] = 0;
+      key[i] = 0;
+      if (p < npkts) {
+        const int4 q = *reinterpret_cast<const int4*>(vparams + 4 * (int64_t)p);   // {frame_len, cr, soft_len, mod}
+        const uint32_t n = (uint32_t)max(q.z, 0);
+        vu[i] = (n + 255u) >> 8;
+        vs[i] = n / (uint32_t)ncbps_of(q.w);
+        key[i] = order_key_of(q.y, q.z);
+      }
+    }
+    if (order) {
+#pragma unroll
+      for (int i = 0; i < kScanPer; i++) order_claim(hist, base + 1024 * i + t < npkts, key[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < kScanPer; i++) { iu[i] = wave_incl_scan(vu[i]); is[i] = wave_incl_scan(vs[i]); }
+    if (lane == 63) {
+#pragma unroll
+      for (int i = 0; i < kScanPer; i++) wtab[16 * i + wv] = make_uint2(iu[i], is[i]);
+    }
+    __syncthreads();
+    if (wv == 0) {                                     // exclusive scan of the 256 totals, 4 per lane
+      uint2 x[4];
+      uint32_t su = 0, ss = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) { x[j] = wtab[4 * lane + j]; su += x[j].x; ss += x[j].y; }
+      uint32_t eu = wave_incl_scan(su) - su, es = wave_incl_scan(ss) - ss;
+#pragma unroll
+      for (int j = 0; j < 4; j++) { wtab[4 * lane + j] = make_uint2(eu, es); eu += x[j].x; es += x[j].y; }
+      if (lane == 63) round_total = make_uint2(eu, es);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kScanPer; i++) {
+      const int p = base + 1024 * i + t;
+      if (p < npkts) {
+        const uint2 e = wtab[16 * i + wv];
+        const uint64_t u0 = carry_u + e.x + iu[i] - vu[i];
+        const uint32_t s0 = carry_s + e.y + is[i] - vs[i], s1 = s0 + vs[i];
+        off[p] = (int64_t)(u0 << 8);
+        dsym[p] = (int32_t)s0;
+        for (uint32_t w = (s0 + 63u) >> 6; 64u * w < s1; w++) wave_p0[w] = p;
+      }
+    }
+    const uint2 rt = round_total;
+    carry_u += rt.x;
+    carry_s += rt.y;
+    __syncthreads();                                   // wtab is rewritten by the next round
   }
-  if ((t & 63) == 63) wsum[t >> 6] = inc;
+  if (t == 0) dsym[npkts] = (int32_t)carry_s;          // the whole batch's data symbols
+  if (!order) return;
+  order_hist_scan(hist);                               // (the round loop ended on a barrier)
   __syncthreads();
-  uint64_t base = inc - mine;
-  for (int w = 0; w < (t >> 6); w++) base += wsum[w];
-  for (int p = lo; p < hi; p++) {
-    const uint64_t it = item(p);
-    const uint32_t s0 = (uint32_t)base, s1 = s0 + (uint32_t)it;
-    off[p] = (int64_t)(base >> 32) << 8;
-    dsym[p] = (int32_t)s0;
-    for (uint32_t w = (s0 + 63u) >> 6; 64u * w < s1; w++) wave_p0[w] = p;
-    base += it;
+  const bool one_round = npkts <= 1024 * kScanPer;
+  for (int base = 0; base < npkts; base += 1024 * kScanPer) {
+    if (!one_round) {
+#pragma unroll
+      for (int i = 0; i < kScanPer; i++) {
+        const int p = base + 1024 * i + t;
+        key[i] = p < npkts ? order_key(vparams, p) : 0u;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kScanPer; i++) {
+      const int p = base + 1024 * i + t;
+      const uint32_t slot = order_claim(hist, p < npkts, key[i]);
+      if (p < npkts) order[slot] = p;
+    }
   }
-  if (t == 1023) dsym[npkts] = (int32_t)(uint32_t)base;   // the whole batch's data symbols
 }
 
-// ------------------------------------------------------------------ data symbols -> soft
 constexpr int kDataFftBlocks = 2048;  // k_data_fft grid cap: 8192 waves, 32 per CU, looping
 
 template <int MOD, bool EQ>
@@ -266,7 +336,7 @@ __device__ __forceinline__ void data_fft_symbol(const uint4* __restrict__ src, i
   if constexpr (EQ) equalize_data_bins(x, [cp](int b) { return as_s2(cp[b]); }, k + 1, T);
   demap_deinterleave_st<MOD>(x, lut, [dst](int q, uint4 v) { dst[q] = v; });
 }
-// Flat over the batch's data symbols (k_soft_scan numbers them): wave w takes symbols
+// Flat over the batch's data symbols (k_pkt_plan numbers them): wave w takes symbols
 // 64w .. 64w+63, lane = symbol, whatever packets they belong to, so a long packet spreads
 // over many waves and consecutive lanes write consecutive soft rows.  Waves loop over w with
 // the grid's stride (the host sizes the grid from the call's max_nsym, an upper bound).

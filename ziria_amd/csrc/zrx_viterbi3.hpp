@@ -772,70 +772,91 @@ __global__ __launch_bounds__(256, 4) void k_viterbi3(const uint8_t* __restrict__
 
 // Packet order for k_viterbi3 over a mixed batch (BASELINE config 5): by code rate, then by
 // trellis length, longest first, so the four rows of a wave share one rate and similar
-// lengths.  One 1024-thread block; counting sort over (rate, 24-column bodies) keys, with
-// runs of equal keys in a thread's contiguous slice counted by one LDS atomic (a uniform
-// batch costs 1024 atomics, not one per packet).  Keys are recomputed from vparams in the
-// scatter pass (no per-packet LDS), so any batch size is ordered; 1024 length buckets cover
-// 24576 columns, i.e. every 802.11a frame (at most 8 x 2050 + 6 = 16406 columns); longer
-// device-API frames share the last bucket.
+// lengths.  One 1024-thread block; counting sort over (rate, 24-column bodies) keys.  Packets
+// are read coalesced (p = 1024 k + thread, 16 loads per thread in flight) and their keys
+// recomputed in the scatter pass, so
+// any batch size is ordered; a wave whose 64 packets share a key (any uniform batch) counts
+// and places them with one LDS atomic.  1024 length buckets cover 24576 columns, i.e. every
+// 802.11a frame (at most 8 x 2050 + 6 = 16406 columns); longer device-API frames share the
+// last bucket.  Within a bucket the order is whatever the atomics give (each packet decodes
+// the same wherever it lands).
 constexpr int kOrderLen = 1024;                        // length buckets of 24 columns
 constexpr int kOrderKeys = 3 * kOrderLen + 1;          // + one bucket for packets with no work
 constexpr int kOrderPerThread = (kOrderKeys + 1023) / 1024;
-__device__ __forceinline__ uint32_t order_key(const int32_t* __restrict__ vparams, int p) {
-  const int32_t* vp = vparams + 4 * (int64_t)p;
-  const int cr = vp[1], n = vp[2];
+__device__ __forceinline__ uint32_t order_key_of(int cr, int n) {
   if (n <= 0 || cr < 0 || cr > 2) return 3u * kOrderLen;
   const uint32_t cols = (uint32_t)(n / (cr == 0 ? 2 : cr == 1 ? 3 : 4)) * (uint32_t)(cr + 1);
   const uint32_t bodies = min((cols + 23u) / 24u, (uint32_t)kOrderLen - 1u);
   return (uint32_t)cr * kOrderLen + (kOrderLen - 1u - bodies);
 }
+__device__ __forceinline__ uint32_t order_key(const int32_t* __restrict__ vparams, int p) {
+  const int32_t* vp = vparams + 4 * (int64_t)p;
+  return order_key_of(vp[1], vp[2]);
+}
+// Adds this wave's valid lanes to hist[key] and returns each lane's slot (old count + rank
+// among the lanes sharing its key): one atomic when the wave's keys agree.
+__device__ __forceinline__ uint32_t order_claim(uint32_t* hist, bool valid, uint32_t key) {
+  const uint64_t mask = __builtin_amdgcn_ballot_w64(valid);
+  if (mask == 0) return 0;
+  const uint32_t first = (uint32_t)__builtin_ctzll(mask);
+  const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)first);
+  if (__builtin_amdgcn_ballot_w64(valid && key == k0) == mask) {
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+    uint32_t base = 0;
+    if ((threadIdx.x & 63u) == first) base = atomicAdd(&hist[k0], (uint32_t)__builtin_popcountll(mask));
+    return (uint32_t)__builtin_amdgcn_readlane((int)base, (int)first) + rank;
+  }
+  return valid ? atomicAdd(&hist[key], 1u) : 0u;
+}
+// hist[] counts -> exclusive starts (1024 threads, kOrderPerThread buckets each); the caller
+// syncs before and after.
+__device__ __forceinline__ void order_hist_scan(uint32_t* hist) {
+  __shared__ uint32_t wsum[16];
+  const int t = threadIdx.x;
+  uint32_t v[kOrderPerThread], mine = 0;
+#pragma unroll
+  for (int j = 0; j < kOrderPerThread; j++) { v[j] = hist[kOrderPerThread * t + j]; mine += v[j]; }
+  uint32_t inc = mine;                                 // inclusive scan inside the wave
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = (uint32_t)__shfl_up((int)inc, o);
+    if ((t & 63) >= o) inc += u;
+  }
+  if ((t & 63) == 63) wsum[t >> 6] = inc;
+  __syncthreads();
+  uint32_t ex = inc - mine;
+  for (int w = 0; w < (t >> 6); w++) ex += wsum[w];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kOrderPerThread; j++) { hist[kOrderPerThread * t + j] = ex; ex += v[j]; }
+}
 __global__ __launch_bounds__(1024) void k_vit_order(const int32_t* __restrict__ vparams, int npkts,
                                                     int32_t* __restrict__ order) {
   __shared__ uint32_t hist[kOrderPerThread * 1024];
-  for (int i = threadIdx.x; i < kOrderPerThread * 1024; i += blockDim.x) hist[i] = 0;
+  const int t = threadIdx.x;
+  for (int i = t; i < kOrderPerThread * 1024; i += blockDim.x) hist[i] = 0;
   __syncthreads();
-  const int per = (npkts + (int)blockDim.x - 1) / (int)blockDim.x;
-  const int lo = min((int)threadIdx.x * per, npkts), hi = min(lo + per, npkts);
-  uint32_t prev = 0xFFFFFFFFu, run = 0;
-  for (int p = lo; p < hi; p++) {
-    const uint32_t k = order_key(vparams, p);
-    if (k == prev) { run++; continue; }
-    if (run) atomicAdd(&hist[prev], run);
-    prev = k; run = 1;
-  }
-  if (run) atomicAdd(&hist[prev], run);
-  __syncthreads();
-  {                                                    // exclusive scan: kOrderPerThread buckets per thread
-    __shared__ uint32_t wsum[16];
-    const int t = threadIdx.x;
-    uint32_t v[kOrderPerThread], mine = 0;
+  constexpr int kPer = 16;                             // keys per thread in flight together
+  for (int b = 0; b < npkts; b += 1024 * kPer) {
+    uint32_t key[kPer];
 #pragma unroll
-    for (int j = 0; j < kOrderPerThread; j++) { v[j] = hist[kOrderPerThread * t + j]; mine += v[j]; }
-    uint32_t inc = mine;                               // inclusive scan inside the wave
+    for (int i = 0; i < kPer; i++) key[i] = b + 1024 * i + t < npkts ? order_key(vparams, b + 1024 * i + t) : 0u;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t u = (uint32_t)__shfl_up((int)inc, o);
-      if ((t & 63) >= o) inc += u;
-    }
-    if ((t & 63) == 63) wsum[t >> 6] = inc;
-    __syncthreads();
-    uint32_t ex = inc - mine;
-    for (int w = 0; w < (t >> 6); w++) ex += wsum[w];
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kOrderPerThread; j++) { hist[kOrderPerThread * t + j] = ex; ex += v[j]; }
+    for (int i = 0; i < kPer; i++) order_claim(hist, b + 1024 * i + t < npkts, key[i]);
   }
   __syncthreads();
-  prev = 0xFFFFFFFFu; run = 0;
-  int start = lo;
-  for (int p = lo; p <= hi; p++) {
-    const uint32_t k = p < hi ? order_key(vparams, p) : 0xFFFFFFFEu;
-    if (k == prev) { run++; continue; }
-    if (run) {
-      const uint32_t base = atomicAdd(&hist[prev], run);
-      for (uint32_t j = 0; j < run; j++) order[base + j] = start + (int)j;
+  order_hist_scan(hist);
+  __syncthreads();
+  for (int b = 0; b < npkts; b += 1024 * kPer) {
+    uint32_t key[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; i++) key[i] = b + 1024 * i + t < npkts ? order_key(vparams, b + 1024 * i + t) : 0u;
+#pragma unroll
+    for (int i = 0; i < kPer; i++) {
+      const int p = b + 1024 * i + t;
+      const uint32_t slot = order_claim(hist, p < npkts, key[i]);
+      if (p < npkts) order[slot] = p;
     }
-    prev = k; run = 1; start = p;
   }
 }
 
