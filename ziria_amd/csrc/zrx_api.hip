@@ -31,6 +31,7 @@ using namespace zrx;
 
 struct zrx_ctx {
   int device = 0;
+  int ncu = 256;                  // compute units (k_vit_order's block placement)
   int crc_blocks = 1024;          // k_descramble_crc grid cap (blocks of kCrcWaves packets)
 #ifdef ZRX_EXPERIMENTS
   // A/B builds only (scripts/build_variant.sh): environment knobs that select other kernels
@@ -311,7 +312,7 @@ static void launch_viterbi(zrx_ctx* c, const uint8_t* soft, const int64_t* soft_
   // workspace has room for it (zrx_reserve); otherwise identity order (still exact)
   const int32_t* order = nullptr;
   if (order_fits(c, npkts)) {
-    if (!order_ready) k_vit_order<<<1, 1024, 0, c->stream>>>(params, npkts, c->order);
+    if (!order_ready) k_vit_order<<<1, 1024, 0, c->stream>>>(params, npkts, c->order, c->ncu);
     order = c->order;
   }
   const dim3 g(blocks(npkts, v3::kRows)), b(256);
@@ -347,6 +348,7 @@ int zrx_create(zrx_ctx** out, int device, void* stream) {
   ZRX_CHECK(hipSetDevice(device));
   zrx_ctx* c = new zrx_ctx();
   c->device = device;
+  ZRX_CHECK(hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device));
   c->stream = (hipStream_t)stream;
 #ifdef ZRX_EXPERIMENTS
   if (const char* v = std::getenv("ZRX_VITERBI")) {
@@ -509,7 +511,8 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
   if (ev) ZRX_CHECK(hipEventRecord(ev[1], s));
   k_signal_vit<<<blocks(npkts, 4), 256, 0, s>>>(c->sig_soft, d_nsym, npkts, c->cap_nsym, c->vparams, d_info);
   const bool ordered = order_fits(c, npkts);
-  k_pkt_plan<<<1, 1024, 0, s>>>(c->vparams, npkts, c->soft_off, c->dsym, c->wave_p0, ordered ? c->order : nullptr);
+  k_pkt_plan<<<1, 1024, 0, s>>>(c->vparams, npkts, c->soft_off, c->dsym, c->wave_p0, ordered ? c->order : nullptr,
+                                c->ncu);
   if (ev) ZRX_CHECK(hipEventRecord(ev[2], s));
   // k_data_fft: waves over the batch's data symbols, at most npkts x (max_nsym - 1) of them
   const int fft_blocks = (int)std::min<int64_t>(((int64_t)npkts * (max_nsym - 1) + 255) / 256, kDataFftBlocks);

@@ -236,7 +236,7 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
 }
 __global__ __launch_bounds__(1024) void k_pkt_plan(const int32_t* __restrict__ vparams, int npkts,
                                                    int64_t* __restrict__ off, int32_t* __restrict__ dsym,
-                                                   int32_t* __restrict__ wave_p0, int32_t* __restrict__ order) {
+                                                   int32_t* __restrict__ wave_p0, int32_t* __restrict__ order, int ncu) {
   __shared__ uint2 wtab[kScanPer * 16];                // (chunk i, wave w) totals, then offsets
   __shared__ uint2 round_total;
   __shared__ uint32_t hist[kOrderPerThread * 1024];
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(1024) void k_pkt_plan(const int32_t* __restrict__ v
     for (int i = 0; i < kScanPer; i++) {
       const int p = base + 1024 * i + t;
       const uint32_t slot = order_claim(hist, p < npkts, key[i]);
-      if (p < npkts) order[slot] = p;
+      if (p < npkts) order[order_place(slot, (uint32_t)npkts >> 4, (uint32_t)ncu)] = p;
     }
   }
 }

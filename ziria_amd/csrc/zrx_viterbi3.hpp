@@ -793,6 +793,19 @@ __device__ __forceinline__ uint32_t order_key(const int32_t* __restrict__ vparam
   const int32_t* vp = vparams + 4 * (int64_t)p;
   return order_key_of(vp[1], vp[2]);
 }
+// Sorted position -> row slot: the nfull whole blocks of 16 rows placed "snake" over ncu
+// CUs: in odd rounds of ncu blocks the order is reversed, so with blocks dealt to CU
+// (slot mod ncu) — what the dispatcher does when every block of the launch is resident
+// (scripts/ubench/hwid.hip) — the CU running one of the longest blocks gets one of the
+// shortest of the next round beside it.  An involution within each round; a partial last
+// block stays in place.
+__device__ __forceinline__ uint32_t order_place(uint32_t pos, uint32_t nfull, uint32_t ncu) {
+  const uint32_t b = pos >> 4;
+  if (b >= nfull) return pos;
+  const uint32_t r = b / ncu, c = b - r * ncu, base = r * ncu;
+  const uint32_t m = min(ncu, nfull - base);
+  return ((r & 1u) ? base + m - 1u - c : b) * 16u + (pos & 15u);
+}
 // Adds this wave's valid lanes to hist[key] and returns each lane's slot (old count + rank
 // among the lanes sharing its key): one atomic when the wave's keys agree.
 __device__ __forceinline__ uint32_t order_claim(uint32_t* hist, bool valid, uint32_t key) {
@@ -831,7 +844,7 @@ __device__ __forceinline__ void order_hist_scan(uint32_t* hist) {
   for (int j = 0; j < kOrderPerThread; j++) { hist[kOrderPerThread * t + j] = ex; ex += v[j]; }
 }
 __global__ __launch_bounds__(1024) void k_vit_order(const int32_t* __restrict__ vparams, int npkts,
-                                                    int32_t* __restrict__ order) {
+                                                    int32_t* __restrict__ order, int ncu) {
   __shared__ uint32_t hist[kOrderPerThread * 1024];
   const int t = threadIdx.x;
   for (int i = t; i < kOrderPerThread * 1024; i += blockDim.x) hist[i] = 0;
@@ -855,7 +868,7 @@ __global__ __launch_bounds__(1024) void k_vit_order(const int32_t* __restrict__ 
     for (int i = 0; i < kPer; i++) {
       const int p = b + 1024 * i + t;
       const uint32_t slot = order_claim(hist, p < npkts, key[i]);
-      if (p < npkts) order[slot] = p;
+      if (p < npkts) order[order_place(slot, (uint32_t)npkts >> 4, (uint32_t)ncu)] = p;
     }
   }
 }
