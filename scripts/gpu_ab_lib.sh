@@ -12,6 +12,6 @@ for r in $(seq ${ROUNDS:-2}); do
     python -c "
 import json
 for l in open('gpurun_out/ab${AB_TAG:-}_${v}_$r.log'):
-    if l.startswith('{'): d=json.loads(l); sm=d.get('stage_ms', {}); print('$v', sm.get('data_viterbi'), sm.get('data_fft_demap'), sm.get('signal_viterbi'), d['ms_per_step'], d['value'], d.get('bit_exact_check', {}).get('payload_match') if 'bit_exact_check' in d else d.get('frames_equal_sent'))"
+    if l.startswith('{'): d=json.loads(l); sm=d.get('stage_ms', {}); print('$v', sm.get('data_viterbi'), sm.get('data_fft_demap'), sm.get('signal_viterbi'), sm.get('descramble_crc'), d['ms_per_step'], d['value'], d.get('bit_exact_check', {}).get('payload_match') if 'bit_exact_check' in d else d.get('frames_equal_sent'))"
   done
 done

@@ -547,13 +547,27 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
     const uint32_t ksm = S == 0 ? 0u : 0xFFFFFFFFu;   // state 0 never leaves 0: zero keystream
     const int n0 = (16 * (int)kScrPhase[S]) % 127;
     const int plen = len - 4;
-    // payload: dword i = decoded bytes 2+4i .. 5+4i
+    // payload: dword i = decoded bytes 2+4i .. 5+4i.  The lane's dwords i = lane + 64k
+    // (k < 8: plen <= 2044) are all loaded before any is used (one memory latency per packet,
+    // not one per iteration); the upper neighbour word comes from lane + 1.
+    uint32_t wv[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      const int i = lane + 64 * k;
+      wv[k] = 4 * i < plen + 4 ? d32[i] : 0u;          // words 0 .. (plen+3)/4 <= 512 of the slot
+    }
     int n = (n0 + 4 * lane) % 127;
-    for (int i = lane; 4 * i < plen; i += 64) {
-      uint32_t v = __builtin_amdgcn_alignbyte(d32[i + 1], d32[i], 2) ^ (scrw[n] & ksm);
-      const int rem = plen - 4 * i;
-      if (rem < 4) v &= (1u << (8 * rem)) - 1u;
-      py32[i] = v;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int i = lane + 64 * k;
+      const uint32_t up = (uint32_t)__shfl_down((int)wv[k], 1);
+      const uint32_t nx = lane == 63 ? (uint32_t)__builtin_amdgcn_readlane((int)wv[k + 1], 0) : up;
+      if (4 * i < plen) {
+        uint32_t v = __builtin_amdgcn_alignbyte(nx, wv[k], 2) ^ (scrw[n] & ksm);
+        const int rem = plen - 4 * i;
+        if (rem < 4) v &= (1u << (8 * rem)) - 1u;
+        py32[i] = v;
+      }
       n += 2;                                          // 256 bytes on: 256 = 2 mod 127
       if (n >= 127) n -= 127;
     }
