@@ -259,7 +259,7 @@ __global__ __launch_bounds__(1024) void k_pkt_plan(const int32_t* __restrict__ v
         const int4 q = *reinterpret_cast<const int4*>(vparams + 4 * (int64_t)p);   // {frame_len, cr, soft_len, mod}
         const uint32_t n = (uint32_t)max(q.z, 0);
         vu[i] = (n + 255u) >> 8;
-        vs[i] = n / (uint32_t)ncbps_of(q.w);
+        vs[i] = q.w == 3 ? n / 288u : (n >> (q.w & 3)) / 48u;   // soft_len / N_CBPS, constant divisors
         key[i] = order_key_of(q.y, q.z);
       }
     }

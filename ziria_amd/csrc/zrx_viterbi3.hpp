@@ -785,7 +785,8 @@ constexpr int kOrderKeys = 3 * kOrderLen + 1;          // + one bucket for packe
 constexpr int kOrderPerThread = (kOrderKeys + 1023) / 1024;
 __device__ __forceinline__ uint32_t order_key_of(int cr, int n) {
   if (n <= 0 || cr < 0 || cr > 2) return 3u * kOrderLen;
-  const uint32_t cols = (uint32_t)(n / (cr == 0 ? 2 : cr == 1 ? 3 : 4)) * (uint32_t)(cr + 1);
+  const uint32_t u = (uint32_t)n;                      // trellis columns, with constant divisors
+  const uint32_t cols = cr == 0 ? u >> 1 : cr == 1 ? (u / 3u) * 2u : (u >> 2) * 3u;
   const uint32_t bodies = min((cols + 23u) / 24u, (uint32_t)kOrderLen - 1u);
   return (uint32_t)cr * kOrderLen + (kOrderLen - 1u - bodies);
 }
