@@ -11,6 +11,6 @@ for r in $(seq ${ROUNDS:-2}); do
     python -c "
 import json
 for l in open('gpurun_out/abenv_${v}_$r.log'):
-    if l.startswith('{'): d=json.loads(l); print('$VAR=$v', d.get('stage_ms', {}).get('data_viterbi'), d['ms_per_step'], d['value'], d.get('bit_exact_check'))"
+    if l.startswith('{'): d=json.loads(l); sm=d.get('stage_ms', {}); print('$VAR=$v', sm.get('data_viterbi'), sm.get('descramble_crc'), d['ms_per_step'], d['value'], (d.get('bit_exact_check') or {}).get('payload_match'))"
   done
 done

@@ -101,6 +101,7 @@ __device__ __forceinline__ void make_consts(Consts& K, uint32_t l, uint32_t rib)
   for (int k = 0; k < 3; k++)
 #pragma unroll
     for (int q = 0; q < 4; q++) K.sa[k][q] = rib * 64u + rev6(rotl6(pos_of(l, q >> 1, q & 1), 2 * k));
+  // (column snapshots use sa[k][0] and the lane-uniform deltas of sa[k][1..3]; tests/vit3_model.py)
   K.sa2w = K.sa[2][0] & ~3u;   // k = 2: dword address of the lane's 4 consecutive bytes (column5)
 }
 
@@ -555,15 +556,17 @@ struct Packet {
         // (rev6(rotl6(p, 4)) sends position bits 0, 1 to ring-index bits 1, 0): one dword store
         *(uint32_t*)(s + K.sa2w) = __builtin_amdgcn_perm(u1, u0, 0x06020400u);
       } else {
-      // one shift per dword: byte 0 by ds_write_b8, byte 2 by ds_write_b8_d16_hi (asm: the
-      // compiler folds (x >> 1) >> 16 back into a second shift)
-      s[K.sa[c >> 3][0]] = (uint8_t)u0;
-      s[K.sa[c >> 3][2]] = (uint8_t)u1;
-      const uint32_t b0 = lds_addr(ring);
-      asm volatile("ds_write_b8_d16_hi %0, %1 offset:%2" ::"v"(b0 + K.sa[c >> 3][1]), "v"(u0),
-                   "i"((c >> 3) * kSlotBytes) : "memory");
-      asm volatile("ds_write_b8_d16_hi %0, %1 offset:%2" ::"v"(b0 + K.sa[c >> 3][3]), "v"(u1),
-                   "i"((c >> 3) * kSlotBytes) : "memory");
+        // The lane's 4 ring bytes differ from its first by lane-uniform amounts (position
+        // bit 0 = half -> ring-index bit 5 - 2k, bit 1 = dword -> bit 4 - 2k, k = C mod 6 / 2),
+        // so one address register serves all four stores through their offsets.  One shift
+        // per dword: byte 0 by ds_write_b8, byte 2 by ds_write_b8_d16_hi.
+        constexpr uint32_t k = (uint32_t)(c >> 3), o = k * kSlotBytes;
+        constexpr uint32_t dh = 32u >> (2 * k), dd = 16u >> (2 * k);
+        const uint32_t a = lds_addr(ring) + K.sa[k][0];
+        asm volatile("ds_write_b8 %0, %1 offset:%2" ::"v"(a), "v"(u0), "i"(o) : "memory");
+        asm volatile("ds_write_b8 %0, %1 offset:%2" ::"v"(a), "v"(u1), "i"(o + dd) : "memory");
+        asm volatile("ds_write_b8_d16_hi %0, %1 offset:%2" ::"v"(a), "v"(u0), "i"(o + dh) : "memory");
+        asm volatile("ds_write_b8_d16_hi %0, %1 offset:%2" ::"v"(a), "v"(u1), "i"(o + dh + dd) : "memory");
       }
     }
     if constexpr (c % RT::steps == 0) {                // group end
