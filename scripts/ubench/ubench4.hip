@@ -180,6 +180,30 @@ SYN(s_add16dpp,
     }                                                                                       \
     out[blockIdx.x * 256 + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;            \
   }
+
+// ---- column5 as the kernel issues it: per dword and, perm (BX), sub (C - BX), add, add_dpp, pk_min
+#define C5TWO(CTRL, LIT)                                                                     \
+  "v_and_b32 %[a0], 0xfffeffff, %[a0]\n\t"                                                 \
+  "v_and_b32 %[a1], 0xfffeffff, %[a1]\n\t"                                                 \
+  "v_perm_b32 %[a4], %[s], %[c], v242\n\t"                                                 \
+  "v_perm_b32 %[a5], %[s], %[c], v243\n\t"                                                 \
+  "v_sub_u32 %[a6], " LIT ", %[a4]\n\t"                                                    \
+  "v_sub_u32 %[a7], " LIT ", %[a5]\n\t"                                                    \
+  "v_add_u32 %[a4], %[a0], %[a4]\n\t"                                                      \
+  "v_add_u32 %[a5], %[a1], %[a5]\n\t"                                                      \
+  "v_add_u32_dpp %[a6], %[a0], %[a6] " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t" \
+  "v_add_u32_dpp %[a7], %[a1], %[a7] " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t" \
+  "v_pk_min_u16 %[a0], %[a4], %[a6]\n\t"                                                   \
+  "v_pk_min_u16 %[a1], %[a5], %[a7]\n\t"
+#define C5ONE(CTRL, LIT)                                                                     \
+  "v_and_b32 %[a0], 0xfffeffff, %[a0]\n\t"                                                 \
+  "v_perm_b32 %[a4], %[s], %[c], v242\n\t"                                                 \
+  "v_sub_u32 %[a6], " LIT ", %[a4]\n\t"                                                    \
+  "v_add_u32 %[a4], %[a0], %[a4]\n\t"                                                      \
+  "v_add_u32_dpp %[a6], %[a0], %[a6] " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t" \
+  "v_pk_min_u16 %[a0], %[a4], %[a6]\n\t"
+COLK(c5_two_dwords, C5TWO)
+COLK(c5_one_dword, C5ONE)
 COLK(c_compiler_order, COLA)
 COLK(c_paired, COLB)
 COLK(c_paired_vperm, COLC)
@@ -195,7 +219,8 @@ int main() {
       {"8: v_mov_b32", s_mov, 8}, {"8: v_min_u32_e32", s_minu32, 8}, {"8: v_sub_u16", s_sub16, 8},
       {"8: v_lshrrev_b32 vgpr", s_lshr, 8}, {"8: v_min_i32", s_mini32, 8}, {"8: v_add_u16_dpp", s_add16dpp, 8},
       {"col x4: compiler order", c_compiler_order, 4}, {"col x4: paired VOP2", c_paired, 4},
-      {"col x4: paired, perm const vgpr", c_paired_vperm, 4}};
+      {"col x4: paired, perm const vgpr", c_paired_vperm, 4},
+      {"col5 x4: two dwords (4 pkts/wave)", c5_two_dwords, 4}, {"col5 x4: one dword (2 pkts/wave)", c5_one_dword, 4}};
   hipDeviceProp_t p;
   hipGetDeviceProperties(&p, 0);
   const int cus = p.multiProcessorCount;
@@ -205,7 +230,7 @@ int main() {
   hipEventCreate(&a);
   hipEventCreate(&b);
   const double ghz = 2.4;
-  for (int wps : {1, 2, 4}) {
+  for (int wps : {1, 2, 3, 4, 8}) {
     const int blocks = cus * wps;
     for (auto& k : ks) {
       k.f<<<blocks, 256>>>(out, 7);
@@ -217,7 +242,7 @@ int main() {
       hipEventElapsedTime(&ms, a, b);
       const double units = (double)wps * ITERS * 4;     // sequence instances per SIMD
       const double cyc = ms * 1e-3 * ghz * 1e9 / units;
-      const int ninst = k.per == 8 ? 8 : 48;            // instructions per instance
+      const int ninst = k.per == 8 ? 8 : (k.f == c5_one_dword ? 24 : 48);   // instructions per instance
       printf("wps=%d %-36s %7.3f ms %7.2f cyc/instance %5.2f cyc/inst\n", wps, k.n, ms, cyc, cyc / ninst);
       fflush(stdout);
     }
