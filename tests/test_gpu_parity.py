@@ -304,6 +304,28 @@ def test_viterbi_order_large_mixed_batch(oracle):
         assert (got[oo[i]:oo[i] + fl[i]] == exp[oo[i]:oo[i] + fl[i]]).all(), i
 
 
+def test_chain_mixed_order_rounds_and_partial_block(engine, oracle):
+    """4100 mixed packets: k_pkt_plan's packet order spans more than one round of CU blocks
+    (snake placement reverses the second) and ends in a partial block of 4 rows; every packet
+    with a valid header decodes to its payload, and a sample equals the oracle."""
+    m = txgen.make_mixed_fast(4100, min_len=64, max_len=700, sigma=3.0, seed=4100, device="cuda")
+    n = m["sym_off"].numel()
+    engine.reserve(n, m["max_nsym"])
+    pay, info = engine.rx(m["sym"], m["sym_off"], m["nsym"], m["max_nsym"])
+    pay, info = pay.cpu().numpy(), info.cpu().numpy()
+    assert (info[:, 4] == 1).all()
+    for i in range(n):
+        assert (pay[i, :m["meta"][i, 2] - 4] == m["payload"][i]).all(), i
+    sample = np.arange(n - 64, n)                          # the partial block and its neighbours
+    soff, sn = m["sym_off"].cpu().numpy(), m["nsym"].cpu().numpy()
+    sym = m["sym"].cpu().numpy()
+    opay, res = oracle.rx_batch_time(sym, soff[sample], sn[sample], nthreads=8)
+    for j, r in enumerate(res):
+        i = sample[j]
+        assert (info[i, 2], info[i, 4]) == (r["len"], r["crc_ok"]), i
+        assert (pay[i, :r["len"] - 4] == opay[j, :r["len"] - 4]).all(), i
+
+
 def test_viterbi_soft_spread_beyond_window():
     """Rows of a wave whose soft values lie more than 4 GiB apart (device API) decode one at a
     time, exactly."""
