@@ -160,6 +160,12 @@ int zrx_viterbi_dev(zrx_ctx* ctx, const int8_t* d_soft, const int64_t* d_soft_of
                     const int32_t* d_params, int npkts, uint8_t* d_out, const int64_t* d_out_off,
                     int32_t* d_out_bits);
 
+/* The Viterbi plan of the context's last zrx_viterbi_dev / zrx_rx_dev launch (synchronizes):
+ * stats2[0] = decoder rows (frames, or their trellis segments when the batch was too small
+ * to fill the GPU), stats2[1] = frames the seam pass re-decoded from a seam whose two
+ * segments disagreed (DESIGN.md "Trellis segments"). */
+int zrx_plan_stats(zrx_ctx* ctx, int32_t* stats2);
+
 /* Full chain; d_sym_off: int64 symbol index of each packet's SIGNAL symbol; d_nsym: int32
  * symbols available per packet; max_nsym: the largest d_nsym, which must fit the reserved
  * workspace (zrx_reserve).  The device never writes past a packet's workspace slot: a packet

@@ -1,0 +1,78 @@
+"""Trellis segments on the CPU (tests/seg_model.py): the segment geometry's invariants, and a
+frame decoded as segments with the seam check and the fix pass equals the oracle's unsplit
+decode bit for bit, at every rate, clean and noisy, including pure-noise frames whose seams
+disagree (so the fix pass really runs)."""
+import numpy as np
+import pytest
+
+from tests import seg_model as SM
+from tests.golden import synth
+
+
+def test_geometry_invariants():
+    for fl in list(range(384, 5000, 37)) + [2050, 4095]:
+        E = 8 * fl + 6
+        for cr in (0, 1, 2):
+            K = (24, 32, 36)[cr]                             # decoded bits per 48 soft values
+            cols = -(-E // K) * K
+            for nseg in range(2, min(SM.MAX_SEG, E // SM.MIN_SEG) + 1):
+                S = [SM.seg_start(E, nseg, k) for k in range(nseg)]
+                assert S[0] == 0 and all(b > a for a, b in zip(S, S[1:]))
+                for k in range(1, nseg):
+                    assert S[k] % 768 == 0 and S[k] >= 768
+                    assert S[k] + SM.WARM + 64 <= E          # window J_k - 256 fires before the frame end
+                    assert (S[k] + SM.CMP) % 24 == 0         # the seam column is a body end
+                for k in range(nseg):
+                    assert SM.seg_stop(E, cols, nseg, k) > S[k] + SM.CMP
+
+
+def test_row_bound():
+    """sum of segments <= batch columns / L + packets for L >= columns / (64 ncu): the grid
+    of k_viterbi3's planned launch (zrx_api.hip plan_rows_max)."""
+    rng = np.random.default_rng(3)
+    for _ in range(200):
+        n = int(rng.integers(1, 3000))
+        fl = rng.integers(1, 4096, n)
+        E = 8 * fl + 6
+        cols = E + rng.integers(0, 300, n)
+        T = int(cols.sum())
+        L = max(SM.MIN_SEG, -(-T // (64 * 256)))
+        Lb = L + L // 8
+        rows = sum(SM.seg_count(int(e), int(c), Lb) for e, c in zip(E, cols))
+        assert rows <= min(n + 64 * 256, n * SM.MAX_SEG)
+
+
+CASES = [(cr, fl, noise, nseg) for cr in (0, 1, 2) for fl, noise, nseg in
+         [(400, 0, 2), (700, 3, 3), (1100, 2, 5), (700, -1, 3), (1100, -1, 5)]]
+
+
+@pytest.mark.parametrize("cr,fl,noise,nseg", CASES)
+def test_segmented_equals_oracle(oracle, cr, fl, noise, nseg):
+    s = synth.viterbi_soft(cr, fl, noise, seed=100 * cr + fl + noise)
+    exp = oracle.viterbi_decode(s, fl, cr)
+    got, fixes = SM.segmented_decode(s, cr, fl, nseg)
+    assert got.size == exp.size == fl
+    assert (got == exp).all()
+    if noise >= 0:
+        assert fixes == 0                                # clean frames converge in the warm-up
+
+
+def test_pure_noise_exercises_fix(oracle):
+    """Pure-noise frames: some seam disagrees, the fix row re-decodes from it, still exact."""
+    fixes = 0
+    for seed in range(6):
+        s = synth.viterbi_soft(2, 900, -1, seed=seed)
+        got, f = SM.segmented_decode(s, 2, 900, 4)
+        assert (got == oracle.viterbi_decode(s, 900, 2)).all(), seed
+        fixes += f
+    assert fixes > 0
+
+
+def test_pure_noise_many_seams(oracle):
+    """Long pure-noise frames cut into 8: several seams disagree, not always next to each
+    other (a fix row that stopped at the first seam it agrees with would leave a later
+    disagreeing segment in place)."""
+    for seed in (7041, 41, 42):                          # 7041: seams 1, 4, 6, 7 disagree
+        s = synth.viterbi_soft(2, 2035, -1, seed=seed)
+        got, _ = SM.segmented_decode(s, 2, 2035, 8)
+        assert (got == oracle.viterbi_decode(s, 2035, 2)).all(), seed

@@ -31,7 +31,7 @@ using namespace zrx;
 
 struct zrx_ctx {
   int device = 0;
-  int ncu = 256;                  // compute units (k_vit_order's block placement)
+  int ncu = 256;                  // compute units (k_pkt_plan: segment length, block placement)
   int crc_blocks = 1024;          // k_descramble_crc grid cap (blocks of kCrcWaves packets)
 #ifdef ZRX_EXPERIMENTS
   // A/B builds only (scripts/build_variant.sh): environment knobs that select other kernels
@@ -56,8 +56,14 @@ struct zrx_ctx {
   uint8_t* dec = nullptr;         // kDecStride B per packet
   int64_t* dec_off = nullptr;     // p * kDecStride
   int32_t* dec_bits = nullptr;
-  int32_t* order = nullptr;       // Viterbi packet order (k_vit_order)
-  bool use_order = true;          // ZRX_ORDER=0 (experiment builds) turns the ordering off
+  // k_viterbi3's row table (k_pkt_plan): segments of the batch's frames in decode order
+  int2* rows = nullptr;           // {packet, k | nseg << 8}, at most rows_cap
+  int32_t* nrows = nullptr;       // rows planned for the current launch
+  uint8_t* segs = nullptr;        // segments per packet
+  int32_t* order = nullptr;       // k_pkt_plan scratch: packets in row order
+  uint2* dumps = nullptr;         // seam metric dumps, v3::seam_index
+  int64_t rows_cap = 0;
+  bool use_order = true;          // ZRX_ORDER=0 (experiment builds) turns the plan off
   // The workspace is shared by every launch of this context: a launch on a different stream
   // than the previous one first waits for the previous launch's work (ws_free).
   hipEvent_t ws_free = nullptr;
@@ -97,10 +103,12 @@ static int check_device(int device) {
 
 static void free_ws(zrx_ctx* c) {
   for (void* p : {(void*)c->sig_soft, (void*)c->vparams, (void*)c->soft, (void*)c->soft_off, (void*)c->dsym,
-                  (void*)c->wave_p0, (void*)c->dec, (void*)c->dec_off, (void*)c->dec_bits, (void*)c->order})
+                  (void*)c->wave_p0, (void*)c->dec, (void*)c->dec_off, (void*)c->dec_bits, (void*)c->rows,
+                  (void*)c->nrows, (void*)c->segs, (void*)c->dumps, (void*)c->order})
     (void)hipFree(p);
   c->sig_soft = nullptr; c->vparams = nullptr; c->soft = nullptr; c->soft_off = nullptr;
-  c->dsym = nullptr; c->wave_p0 = nullptr; c->dec = nullptr; c->dec_off = nullptr; c->dec_bits = nullptr; c->order = nullptr;
+  c->dsym = nullptr; c->wave_p0 = nullptr; c->dec = nullptr; c->dec_off = nullptr; c->dec_bits = nullptr;
+  c->rows = nullptr; c->nrows = nullptr; c->segs = nullptr; c->dumps = nullptr; c->order = nullptr; c->rows_cap = 0;
   c->cap_pkts = c->cap_nsym = 0;
 }
 
@@ -287,7 +295,7 @@ static bool order_fits(const zrx_ctx* c, int npkts) {
 #ifdef ZRX_EXPERIMENTS
   if (c->vit_impl != 3) return false;
 #endif
-  return c->use_order && c->order && npkts <= c->cap_pkts;
+  return c->use_order && c->rows && npkts <= c->cap_pkts;
 }
 
 // Every launch function starts here: a launch on a different stream than the previous one
@@ -304,18 +312,28 @@ static int ws_release(zrx_ctx* c) {
   return ZRX_OK;
 }
 
-// order_ready: the caller already wrote the packet order into c->order (rx chain: k_pkt_plan)
+// Rows a plan of npkts packets can have: sum of ceil(cols / L) <= total / L + npkts with
+// total / L <= 64 ncu (k_pkt_plan), and at most kMaxSeg per packet.
+static int64_t plan_rows_max(const zrx_ctx* c, int npkts) {
+  return std::min<int64_t>((int64_t)npkts + 64 * (int64_t)c->ncu, (int64_t)npkts * v3::kMaxSeg);
+}
+
+// planned: the caller already ran k_pkt_plan for this batch (rx chain)
 static void launch_viterbi(zrx_ctx* c, const uint8_t* soft, const int64_t* soft_off, const int32_t* params,
                            int npkts, uint8_t* out, const int64_t* out_off, int32_t* out_bits,
-                           bool order_ready = false) {
-  // rows of a k_viterbi3 wave should share a rate and length: order the batch first when the
-  // workspace has room for it (zrx_reserve); otherwise identity order (still exact)
-  const int32_t* order = nullptr;
-  if (order_fits(c, npkts)) {
-    if (!order_ready) k_vit_order<<<1, 1024, 0, c->stream>>>(params, npkts, c->order, c->ncu);
-    order = c->order;
-  }
-  const dim3 g(blocks(npkts, v3::kRows)), b(256);
+                           bool planned = false) {
+  // rows of a k_viterbi3 wave should share a rate and length, and long frames are cut into
+  // segments when the batch is too small to fill the GPU: plan the batch first when the
+  // workspace has room for it (zrx_reserve); otherwise one row per packet in batch order
+  // (still exact)
+  const bool plan = order_fits(c, npkts);
+  if (plan && !planned)
+    k_pkt_plan<<<1, 1024, 0, c->stream>>>(params, npkts, nullptr, nullptr, nullptr, c->rows, c->nrows, c->segs, c->order,
+                                          out_bits, c->ncu);
+  const dim3 b(256);
+  const dim3 g(blocks(plan ? plan_rows_max(c, npkts) : npkts, v3::kRows));
+  const int2* rows = plan ? c->rows : nullptr;
+  int32_t* nrows = plan ? c->nrows : nullptr;
 #ifdef ZRX_EXPERIMENTS
   if (c->vit_impl == 1) {
     k_viterbi<<<blocks(npkts, 4), 256, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits, 256);
@@ -326,14 +344,20 @@ static void launch_viterbi(zrx_ctx* c, const uint8_t* soft, const int64_t* soft_
     return;
   }
   switch (c->v3dbg) {   // timing experiments (ZRX_V3DBG); 0 is the product kernel
-#define ZRX_V3(D) case D: k_viterbi3<D><<<g, b, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits, order); return;
+#define ZRX_V3(D) case D: k_viterbi3<D><<<g, b, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits, rows, nrows, nullptr, c->dumps); return;
     ZRX_V3(1) ZRX_V3(2) ZRX_V3(4) ZRX_V3(8) ZRX_V3(16) ZRX_V3(32) ZRX_V3(64) ZRX_V3(128) ZRX_V3(256) ZRX_V3(512)
     ZRX_V3(1024) ZRX_V3(1032)
 #undef ZRX_V3
     default: break;
   }
 #endif
-  k_viterbi3<0><<<g, b, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits, order);
+  k_viterbi3<0><<<g, b, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits, rows, nrows, nullptr,
+                                        c->dumps);
+  // the seam pass: packets whose segments disagree at a seam are re-decoded from there
+  // (normally none; a block-stride grid of at most 2 blocks per CU)
+  if (plan)
+    k_viterbi3<0, true><<<std::min(blocks(npkts, v3::kRows), 2 * c->ncu), b, 0, c->stream>>>(
+        soft, soft_off, params, npkts, out, out_off, out_bits, nullptr, c->nrows, c->segs, c->dumps);
 }
 
 extern "C" {
@@ -441,7 +465,12 @@ int zrx_reserve(zrx_ctx* c, int npkts, int max_nsym) {
   ZRX_CHECK(hipMalloc(&c->dec, (size_t)np * kDecStride + 256));
   ZRX_CHECK(hipMalloc(&c->dec_off, (size_t)np * 8 + 8));
   ZRX_CHECK(hipMalloc(&c->dec_bits, (size_t)np * 4 + 4));
-  ZRX_CHECK(hipMalloc(&c->order, (size_t)np * 4 + 4));
+  c->rows_cap = plan_rows_max(c, np);
+  ZRX_CHECK(hipMalloc(&c->rows, (size_t)c->rows_cap * 8 + 8));
+  ZRX_CHECK(hipMalloc(&c->nrows, 16));
+  ZRX_CHECK(hipMalloc(&c->segs, (size_t)np + 16));
+  ZRX_CHECK(hipMalloc(&c->order, (size_t)np * 4 + 16));
+  ZRX_CHECK(hipMalloc(&c->dumps, (size_t)np * (v3::kMaxSeg - 1) * 2 * v3::kSeamWords * 8 + 256));
   if (np > 0) {
     k_fill_offsets<<<blocks(np, 256), 256, 0, c->stream>>>(c->soft_off, np, stride);
     k_fill_offsets<<<blocks(np, 256), 256, 0, c->stream>>>(c->dec_off, np, kDecStride);
@@ -449,6 +478,15 @@ int zrx_reserve(zrx_ctx* c, int npkts, int max_nsym) {
   }
   ZRX_CHECK(hipStreamSynchronize(c->stream));
   c->cap_pkts = np; c->cap_nsym = ns; c->soft_stride = stride;
+  return ZRX_OK;
+}
+
+int zrx_plan_stats(zrx_ctx* c, int32_t* stats2) {
+  if (!c || !stats2) return ZRX_EINVAL;
+  stats2[0] = stats2[1] = 0;
+  if (!c->nrows) return ZRX_OK;
+  ZRX_CHECK(hipMemcpyAsync(stats2, c->nrows, 8, hipMemcpyDeviceToHost, c->stream));
+  ZRX_CHECK(hipStreamSynchronize(c->stream));
   return ZRX_OK;
 }
 
@@ -464,6 +502,16 @@ int zrx_viterbi_dev(zrx_ctx* c, const int8_t* d_soft, const int64_t* d_soft_off,
                     int npkts, uint8_t* d_out, const int64_t* d_out_off, int32_t* d_out_bits) {
   if (!c || npkts < 0) return ZRX_EINVAL;
   if (npkts == 0) return ZRX_OK;
+#ifdef ZRX_GUARD
+  {
+    const char* ob = std::getenv("ZRX_GUARD_OUT");
+    const uint64_t lo = (uint64_t)(uintptr_t)d_out, hi = lo + (ob ? std::strtoull(ob, nullptr, 10) : 0ull);
+    const uint32_t np = (uint32_t)npkts;
+    ZRX_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(v3::g_zg_out_lo), &lo, 8));
+    ZRX_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(v3::g_zg_out_hi), &hi, 8));
+    ZRX_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(v3::g_zg_np), &np, 4));
+  }
+#endif
   const int rc = ws_acquire(c);
   if (rc) return rc;
   launch_viterbi(c, (const uint8_t*)d_soft, d_soft_off, d_params, npkts, d_out, d_out_off, d_out_bits);
@@ -511,8 +559,8 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
   if (ev) ZRX_CHECK(hipEventRecord(ev[1], s));
   k_signal_vit<<<blocks(npkts, 4), 256, 0, s>>>(c->sig_soft, d_nsym, npkts, c->cap_nsym, c->vparams, d_info);
   const bool ordered = order_fits(c, npkts);
-  k_pkt_plan<<<1, 1024, 0, s>>>(c->vparams, npkts, c->soft_off, c->dsym, c->wave_p0, ordered ? c->order : nullptr,
-                                c->ncu);
+  k_pkt_plan<<<1, 1024, 0, s>>>(c->vparams, npkts, c->soft_off, c->dsym, c->wave_p0, ordered ? c->rows : nullptr,
+                                c->nrows, c->segs, c->order, c->dec_bits, c->ncu);
   if (ev) ZRX_CHECK(hipEventRecord(ev[2], s));
   // k_data_fft: waves over the batch's data symbols, at most npkts x (max_nsym - 1) of them
   const int fft_blocks = (int)std::min<int64_t>(((int64_t)npkts * (max_nsym - 1) + 255) / 256, kDataFftBlocks);
@@ -873,7 +921,7 @@ int32_t __ext_viterbi_batch_decode(int8_t* soft, int softlen, int32_t* pkt_soft_
   }
   std::lock_guard<std::mutex> lk(g_mu);
   zrx_ctx* c = default_ctx();
-  int rc0 = zrx_reserve(c, np, 1);                   // room for the packet order of k_vit_order
+  int rc0 = zrx_reserve(c, np, 1);                   // room for the row plan of k_pkt_plan
   if (rc0) return rc0;
   const size_t s_soft = ((size_t)softlen + 255) / 256 * 256, s_par = (size_t)np * 16, s_off = (size_t)np * 8;
   const size_t s_out = ((size_t)out_bytes + 255) / 256 * 256;

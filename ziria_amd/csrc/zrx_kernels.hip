@@ -209,22 +209,32 @@ __global__ __launch_bounds__(256) void k_signal_vit(const uint32_t* __restrict__
   }
 }
 
-// The rx chain's per-batch plan, from what each packet's header asks for (vparams,
-// k_signal_vit), in one kernel right after it:
+// The per-batch plan, from what each packet's header asks for (vparams, k_signal_vit), in
+// one kernel right after it:
 //   off[p]       = sum over q < p of soft_len(q) rounded up to 256 B (packed soft slots: a
 //                  batch's soft values stay within the Viterbi's 4 GiB read window, which a
 //                  mixed batch sized for its longest packet at 64-QAM would not);
 //   dsym[p]      = sum over q < p of the data symbols of q; dsym[npkts] = all of them;
 //   wave_p0[w]   = the packet holding batch data symbol 64w (k_data_fft's waves);
-//   order        = k_viterbi3's packet order (k_vit_order's counting sort, same keys), when
-//                  not null.
+//   rows, nrows  = k_viterbi3's row table when rows is not null: every packet cut into
+//                  segs[p] trellis segments (zrx_viterbi3.hpp) of about L columns, L = the
+//                  batch's columns / (64 rows per CU x ncu), so a batch of few or unequal
+//                  frames still gives every SIMD four waves (a batch of equal frames that
+//                  already does, e.g. BASELINE config 3, is not cut); the rows ordered by
+//                  (rate, segment length) — the segments of a packet on consecutive rows —
+//                  and placed snake over the CUs; a packet with no trellis columns (header
+//                  error, truncated) gets no row and out_bits[p] = 0.  order[]: scratch.
+// off null: rows only (the Viterbi device API, whose soft offsets are the caller's).
 // One 1024-thread block, rounds of 16 x 1024 packets: every thread loads its 16 packets'
 // parameters (p = round base + 1024 i + thread: coalesced, all loads in flight together),
 // 16 independent DPP wave scans of the two 32-bit sums (256-B units, symbols), one table of
-// 256 (chunk, wave) offsets scanned by wave 0, every thread's 16 offsets from it; the order
-// keys are counted in the same pass and scattered in a second one.  (As separate kernels,
-// the order ran on a side stream and its join, with the fork, cost ~45 us per step.)
+// 256 (chunk, wave) offsets scanned by wave 0, every thread's 16 offsets from it; then the
+// segment length from the batch's column total, the packet keys counted in one pass and
+// scattered in another, and the rows expanded from the sorted packets by a block scan.
 constexpr int kScanPer = 16;
+#ifndef ZRX_PLAN_CUT
+#define ZRX_PLAN_CUT 99   // (scripts/ubench/plan_ubench.hip: time k_pkt_plan up to one of its phases)
+#endif
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);   // row_shr:1
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);   // row_shr:2
@@ -234,39 +244,84 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
   return x;
 }
+// Packets in row order: every packet with trellis columns is cut into nseg segments
+// (v3::seg_count) and keyed by (rate, segment length); the counting pass writes segs[p] (and
+// out_bits[p] = 0 for a packet with no columns, which gets no row) and counts keys and rows,
+// the scatter pass writes order[] (packets sorted by key).
+template <bool SCATTER>
+__device__ __forceinline__ void plan_pkts(const int32_t* __restrict__ vparams, int npkts, uint32_t L, uint32_t* hist,
+                                          int32_t* __restrict__ order, uint8_t* __restrict__ segs,
+                                          int32_t* __restrict__ out_bits, uint32_t* nrows_total) {
+  const int t = threadIdx.x;
+  uint32_t my_rows = 0;
+  for (int base = 0; base < npkts; base += 1024 * kScanPer) {
+    int4 q[kScanPer];
+#pragma unroll
+    for (int i = 0; i < kScanPer; i++) {
+      const int p = base + 1024 * i + t;
+      q[i] = p < npkts ? *reinterpret_cast<const int4*>(vparams + 4 * (int64_t)p) : make_int4(0, -1, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < kScanPer; i++) {
+      const int p = base + 1024 * i + t;
+      const bool valid = p < npkts;
+      const uint32_t cols = cols_of(q[i].y, q[i].z);
+      const uint32_t E = q[i].x < 0 || q[i].x > (1 << 21) ? 0xFFFFFFFFu : (uint32_t)q[i].x * 8u + 6u;
+      const uint32_t nseg = SCATTER ? (valid ? (uint32_t)segs[p] : 0u) : cols ? v3::seg_count(E, cols, L) : 0u;
+      if (!SCATTER && valid) {
+        segs[p] = (uint8_t)nseg;
+        if (nseg == 0) out_bits[p] = 0;
+        my_rows += nseg;
+      }
+      // segment length: about cols / nseg, plus the seam overlap
+      const uint32_t len = nseg <= 1u ? cols : v3::udiv_small(min(cols, (1u << 20) - 1u) + nseg - 1u, nseg) + 286u;
+      const uint32_t slot = order_claim(hist, valid && nseg > 0u, order_key_len(q[i].y, len));
+      if (SCATTER && valid && nseg > 0u) order[slot] = p;
+    }
+  }
+  if (!SCATTER) {
+    for (int o = 32; o > 0; o >>= 1) my_rows += (uint32_t)__shfl_xor((int)my_rows, o);
+    if ((t & 63) == 0) atomicAdd(nrows_total, my_rows);
+  }
+}
 __global__ __launch_bounds__(1024) void k_pkt_plan(const int32_t* __restrict__ vparams, int npkts,
                                                    int64_t* __restrict__ off, int32_t* __restrict__ dsym,
-                                                   int32_t* __restrict__ wave_p0, int32_t* __restrict__ order, int ncu) {
+                                                   int32_t* __restrict__ wave_p0, int2* __restrict__ rows,
+                                                   int32_t* __restrict__ nrows, uint8_t* __restrict__ segs,
+                                                   int32_t* __restrict__ order, int32_t* __restrict__ out_bits, int ncu) {
   __shared__ uint2 wtab[kScanPer * 16];                // (chunk i, wave w) totals, then offsets
   __shared__ uint2 round_total;
   __shared__ uint32_t hist[kOrderPerThread * 1024];
+  __shared__ unsigned long long tcols;
+  __shared__ uint32_t rtotal, uniform;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  if (order) {
+  if (rows) {
     for (int i = t; i < kOrderPerThread * 1024; i += 1024) hist[i] = 0;
+    if (t == 0) { tcols = 0; rtotal = 0; uniform = 1; }
     __syncthreads();
   }
   uint64_t carry_u = 0;                                // 256-B units before this round
   uint32_t carry_s = 0;                                // symbols before this round
-  uint32_t key[kScanPer];                              // the last round's keys (the only round up to 16384 packets)
+  uint64_t my_cols = 0;                                // trellis columns of this thread's packets
+  // a uniform batch: every packet asks for the same frame length, rate and soft count
+  const int4 q0 = npkts > 0 ? *reinterpret_cast<const int4*>(vparams) : make_int4(0, 0, 0, 0);
+  bool same = cols_of(q0.y, q0.z) > 0;
   for (int base = 0; base < npkts; base += 1024 * kScanPer) {
     uint32_t vu[kScanPer], vs[kScanPer], iu[kScanPer], is[kScanPer];
 #pragma unroll
     for (int i = 0; i < kScanPer; i++) {
       const int p = base + 1024 * i + t;
       vu[i] = vs[i] = 0;
-      key[i] = 0;
       if (p < npkts) {
         const int4 q = *reinterpret_cast<const int4*>(vparams + 4 * (int64_t)p);   // {frame_len, cr, soft_len, mod}
         const uint32_t n = (uint32_t)max(q.z, 0);
         vu[i] = (n + 255u) >> 8;
         vs[i] = q.w == 3 ? n / 288u : (n >> (q.w & 3)) / 48u;   // soft_len / N_CBPS, constant divisors
-        key[i] = order_key_of(q.y, q.z);
+        my_cols += cols_of(q.y, q.z);
+        same = same && q.x == q0.x && q.y == q0.y && q.z == q0.z;
       }
     }
-    if (order) {
-#pragma unroll
-      for (int i = 0; i < kScanPer; i++) order_claim(hist, base + 1024 * i + t < npkts, key[i]);
-    }
+    if (!off) continue;
 #pragma unroll
     for (int i = 0; i < kScanPer; i++) { iu[i] = wave_incl_scan(vu[i]); is[i] = wave_incl_scan(vs[i]); }
     if (lane == 63) {
@@ -302,25 +357,73 @@ __global__ __launch_bounds__(1024) void k_pkt_plan(const int32_t* __restrict__ v
     carry_s += rt.y;
     __syncthreads();                                   // wtab is rewritten by the next round
   }
-  if (t == 0) dsym[npkts] = (int32_t)carry_s;          // the whole batch's data symbols
-  if (!order) return;
-  order_hist_scan(hist);                               // (the round loop ended on a barrier)
+  if (off && t == 0) dsym[npkts] = (int32_t)carry_s;   // the whole batch's data symbols
+  if (!rows || ZRX_PLAN_CUT <= 1) return;
+  for (int o = 32; o > 0; o >>= 1) my_cols += (uint64_t)__shfl_xor((long long)my_cols, o);
+  if (lane == 0) atomicAdd(&tcols, (unsigned long long)my_cols);
+  if (!same) uniform = 0;
   __syncthreads();
-  const bool one_round = npkts <= 1024 * kScanPer;
-  for (int base = 0; base < npkts; base += 1024 * kScanPer) {
-    if (!one_round) {
-#pragma unroll
-      for (int i = 0; i < kScanPer; i++) {
-        const int p = base + 1024 * i + t;
-        key[i] = p < npkts ? order_key(vparams, p) : 0u;
-      }
+  const uint64_t rt = 64ull * (uint64_t)max(ncu, 1);   // rows that give every SIMD four waves
+  const uint32_t L = (uint32_t)min<uint64_t>(max<uint64_t>((tcols + rt - 1) / rt, v3::kMinSeg), 0xFFFFFFFFull);
+  // (a frame is cut only when it is more than L + L / 8 long: a batch of equal frames just
+  // short of four waves per SIMD stays whole)
+  const uint32_t Lb = L + L / 8u;
+  if (uniform) {                                       // no sort: k_viterbi3 derives each row's segment
+    if (t == 0) {
+      const uint32_t E0 = q0.x > (1 << 21) ? 0xFFFFFFFFu : (uint32_t)q0.x * 8u + 6u;
+      const uint32_t n0 = v3::seg_count(E0, cols_of(q0.y, q0.z), Lb);
+      nrows[v3::kPlanRows] = (int32_t)((uint32_t)npkts * n0);
+      nrows[v3::kPlanFixes] = 0;
+      nrows[v3::kPlanUniform] = (int32_t)n0;
+      nrows[v3::kPlanNcu] = ncu;
     }
+    return;
+  }
+  if (ZRX_PLAN_CUT <= 2) return;
+  plan_pkts<false>(vparams, npkts, Lb, hist, order, segs, out_bits, &rtotal);
+  __syncthreads();
+  if (ZRX_PLAN_CUT <= 3) return;
+  const uint32_t npk = order_hist_scan(hist);          // packets with rows
+  __syncthreads();
+  plan_pkts<true>(vparams, npkts, Lb, hist, order, segs, out_bits, nullptr);
+  __syncthreads();                                     // order[] and segs[] written by the block
+  if (ZRX_PLAN_CUT <= 5) return;
+  // Expand: the segments of the packet at sorted position i are rows prefix(i) .. +nseg - 1
+  // (consecutive, so a wave holds segments of one or two packets of similar length), placed
+  // snake over the CUs.  Thread t takes positions 16t .. 16t + 15 of each round.
+  const uint32_t total = rtotal, nfull = total >> 4;
+  const uint32_t ncu2 = (uint32_t)max(ncu, 2), ncu_rcp = 0xFFFFFFFFu / ncu2 + 1u;
+  __shared__ uint32_t esum[16];
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < npk; base += 1024u * kScanPer) {
+    int32_t pk[kScanPer];
+    uint32_t ns[kScanPer], sum = 0;
 #pragma unroll
     for (int i = 0; i < kScanPer; i++) {
-      const int p = base + 1024 * i + t;
-      const uint32_t slot = order_claim(hist, p < npkts, key[i]);
-      if (p < npkts) order[order_place(slot, (uint32_t)npkts >> 4, (uint32_t)ncu)] = p;
+      const uint32_t pos = base + kScanPer * (uint32_t)t + i;
+      pk[i] = pos < npk ? order[pos] : -1;
     }
+#pragma unroll
+    for (int i = 0; i < kScanPer; i++) { ns[i] = pk[i] >= 0 ? segs[pk[i]] : 0u; sum += ns[i]; }
+    const uint32_t inc = wave_incl_scan(sum);
+    if (lane == 63) esum[wv] = inc;
+    __syncthreads();
+    uint32_t ex = carry + inc - sum, rnd = 0;
+    for (int w = 0; w < 16; w++) { ex += w < wv ? esum[w] : 0u; rnd += esum[w]; }
+#pragma unroll
+    for (int i = 0; i < kScanPer; i++) {
+      for (uint32_t k = 0; k < ns[i]; k++)
+        rows[v3::order_place(ex + k, nfull, ncu2, ncu_rcp)] = make_int2(pk[i], (int)(k | (ns[i] << 8)));
+      ex += ns[i];
+    }
+    carry += rnd;
+    __syncthreads();                                   // esum is rewritten by the next round
+  }
+  if (t == 0) {
+    nrows[v3::kPlanRows] = (int32_t)total;
+    nrows[v3::kPlanFixes] = 0;                         // counted by the seam pass
+    nrows[v3::kPlanUniform] = 0;
+    nrows[v3::kPlanNcu] = (int32_t)ncu2;
   }
 }
 

@@ -264,7 +264,18 @@ __device__ __forceinline__ int64_t rl64(int64_t v, int lane) {
   return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), lane) << 32) |
                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane));
 }
-constexpr int64_t kSoftWindow = 0xFFFFFF00;           // span of one buffer window over soft values
+constexpr int64_t kSoftWindow = 0xFFFFFF00;
+
+// ZRX_GUARD builds (debugging only, scripts/build_guard.sh): every global store of the
+// Viterbi is range-checked against the output buffer the host registered, and a violation
+// is printed and skipped instead of faulting.
+#ifdef ZRX_GUARD
+__device__ uint64_t g_zg_out_lo, g_zg_out_hi;
+__device__ uint32_t g_zg_np;
+#define ZG_OUT_BAD(lo, hi) ((uint64_t)(uintptr_t)(lo) < g_zg_out_lo || (uint64_t)(uintptr_t)(hi) > g_zg_out_hi)
+#else
+#define ZG_OUT_BAD(lo, hi) false
+#endif           // span of one buffer window over soft values
 
 // Rate tables: steps per group, soft values per group, soft values per 24-column body.
 template <int CR> struct Rate;
@@ -272,9 +283,91 @@ template <> struct Rate<0> { static constexpr int steps = 1, G = 2, chunk = 48; 
 template <> struct Rate<1> { static constexpr int steps = 2, G = 3, chunk = 36; };   // 2/3
 template <> struct Rate<2> { static constexpr int steps = 3, G = 4, chunk = 32; };   // 3/4
 
-// Per-row decoder state (row-uniform values in VGPRs).
+// ---- Trellis segments -------------------------------------------------------------------
+// A long frame is decoded as nseg segments side by side (rows of their own), so a batch of
+// few or unequal frames still fills every SIMD.  Segment k >= 1 starts at column
+// S_k = 768 m_k (768 = lcm of the 24-column body and the 256-bit window) from all-zero
+// metrics and owns the output windows from J_k = S_k + 256 on; segment k - 1 runs on until
+// it has written the window ending at J_k (the window at ob = J_k - 256 fires at the first
+// group end with tr >= J_k + 30).  The future of the brick loop depends on the column, the
+// window schedule (ob) and the even parts H of the 64 metrics only (viterbicore.hpp:105-168:
+// the marker LSB is masked off before every add, normalize subtracts min & 0xFE), and the
+// tracebacks of windows from J_k on read decisions of columns > J_k only.  So if both
+// segments hold the same normalized H vector at the seam column C_k = S_k + 240 (a body end,
+// after 240 warm-up columns), every output bit of segment k equals the unsplit decode's.
+// Both sides store their metrics at C_k (the seam "dumps"); a second pass (fix) compares
+// them and, for the first seam of a frame that disagrees, re-decodes from C_k with segment
+// k - 1's exact register state, until it agrees with a later segment's start state (or to
+// the frame's end).  Bit-exact either way; warm-up from zero converges in < 100 columns on
+// every chain input measured, so the fix pass normally finds nothing to do.
+constexpr uint32_t kSegUnit = 768;
+constexpr uint32_t kSegWarm = 256;                     // S_k -> J_k
+constexpr uint32_t kSegCmp = 240;                      // S_k -> C_k
+constexpr int kMaxSeg = 8;
+constexpr uint32_t kMinSeg = 1536;                     // columns per segment at least
+constexpr uint32_t kSegMaxEnd = 1u << 24;              // longer frames are not split
+constexpr uint32_t kSeamWords = 32;                    // uint2 per dump: 16 lanes x (M0, M1)
+
+// floor(y / n) for n = 1..8 and y < 2^20 by a reciprocal multiply (exact there: the error
+// term y / 2^32 stays below the 1/8 gap to the next integer)
+__host__ __device__ __forceinline__ uint32_t udiv_small(uint32_t y, uint32_t n) {
+  return n <= 1u ? y : (uint32_t)(((uint64_t)y * (0xFFFFFFFFu / n + 1u)) >> 32);
+}
+// floor(b / d) for b < 2^20 and 2 <= d < 4096 with rcp = 0xFFFFFFFF / d + 1 (exact: the
+// error term b / 2^32 stays below the 1 / d gap to the next integer)
+__host__ __device__ __forceinline__ uint32_t udiv_rcp(uint32_t b, uint32_t rcp) {
+  return (uint32_t)(((uint64_t)b * rcp) >> 32);
+}
+// Sorted position -> row slot: the nfull whole blocks of 16 rows placed "snake" over ncu
+// CUs: in odd rounds of ncu blocks the order is reversed, so with blocks dealt to CU
+// (slot mod ncu) — what the dispatcher does when every block of the launch is resident
+// (scripts/ubench/hwid.hip) — the CU running one of the longest blocks gets one of the
+// shortest of the next round beside it.  An involution within each round; a partial last
+// block stays in place.  rcp = 0xFFFFFFFF / ncu + 1 (ncu >= 2).
+__host__ __device__ __forceinline__ uint32_t order_place(uint32_t pos, uint32_t nfull, uint32_t ncu, uint32_t rcp) {
+  const uint32_t b = pos >> 4;
+  if (b >= nfull) return pos;
+  const uint32_t r = udiv_rcp(b, rcp), c = b - r * ncu, base = r * ncu;
+  const uint32_t m = min(ncu, nfull - base);
+  return ((r & 1u) ? base + m - 1u - c : b) * 16u + (pos & 15u);
+}
+// The plan header k_pkt_plan writes for k_viterbi3 (int32 words of the nrows buffer).
+enum PlanWord { kPlanRows = 0, kPlanFixes = 1, kPlanUniform = 2, kPlanNcu = 3 };
+
+// start unit m_k of segment k >= 1 of nseg over a frame of E = 8 len + 6 columns (rounded
+// k E / nseg; with E / nseg >= kMinSeg the m_k are distinct and S_k + 256 + 64 <= E)
+__host__ __device__ __forceinline__ uint32_t seg_start(uint32_t E, uint32_t nseg, uint32_t k) {
+  // floor(x / (1536 nseg)) = floor(floor(x / 1536) / nseg)
+  return k == 0 ? 0u : kSegUnit * udiv_small((2u * k * E + nseg * kSegUnit) / (2u * kSegUnit), nseg);
+}
+// segments for a frame of E columns with cols columns of input, target length L
+__host__ __device__ __forceinline__ uint32_t seg_count(uint32_t E, uint32_t cols, uint32_t L) {
+  if (cols < E || E > kSegMaxEnd || E < 2u * kMinSeg || L == 0) return 1u;
+  uint32_t n = (cols + L - 1u) / L;
+  n = min(n, E / kMinSeg);
+  return min(max(n, 1u), (uint32_t)kMaxSeg);
+}
+// first column after segment k (absolute): where segment k + 1's first window is written
+__host__ __device__ __forceinline__ uint32_t seg_stop(uint32_t E, uint32_t cols, uint32_t nseg, uint32_t k) {
+  return k + 1u < nseg ? seg_start(E, nseg, k + 1u) + kSegWarm + 30u : cols;
+}
+// dump of seam j (1 <= j < nseg) of packet p, side 0 (segment j - 1) or 1 (segment j)
+__host__ __device__ __forceinline__ size_t seam_index(uint32_t p, uint32_t j, uint32_t side) {
+  return (((size_t)p * (kMaxSeg - 1) + (j - 1u)) * 2u + side) * kSeamWords;
+}
+
+// Cold per-row facts for the seam events, one entry per row of the block (LDS).
+struct RowX {
+  uint32_t p;                                          // packet
+  uint32_t kn;                                         // k | nseg << 8 | fix << 16 | matched << 17 | seam j << 20
+  uint32_t S, E;                                       // first column (absolute), 8 len + 6
+};
+
+// Per-row decoder state (row-uniform values in VGPRs).  Columns are relative to the row's
+// first column S (a multiple of 24, so body phases are the frame's own).
 struct Row {
   uint32_t ob, end, cols, next;       // output bits so far, 8*frame_len+6, columns of input, next event column
+  uint32_t evc;                       // next seam event column (kNever: none)
   bool live;                          // still decoding (not done, input not exhausted)
   bool ppend, fpend;                  // partial / final traceback due at the body end
   uint32_t pT, plook, fT, fcnt, flook;
@@ -284,7 +377,50 @@ struct Row {
 
 __device__ __forceinline__ uint32_t row_next(const Row& R) {
   if (!R.live) return kNever;
-  return min(min(R.ob + 286u, R.end), R.cols);
+  return min(min(R.ob + 286u, R.end), min(R.cols, R.evc));
+}
+
+// Seam event of a row at relative column tr (a body end, after normalize): a segment stores
+// its metrics for the fix pass; a fix row compares its own with the next segment's start
+// state and, when they agree, stops where that segment's windows begin.
+__device__ __forceinline__ void seam_event(Row& R, uint32_t tr, uint32_t M0, uint32_t M1, uint32_t l, uint32_t rib,
+                                        RowX* rowx, uint2* __restrict__ dumps) {
+  RowX x = rowx[rib];
+  const uint32_t k = x.kn & 0xFFu, nseg = (x.kn >> 8) & 0xFFu, fix = (x.kn >> 16) & 1u, j = x.kn >> 20;
+  (void)tr;
+#ifdef ZRX_GUARD
+  if (x.p >= g_zg_np || j == 0 || j >= nseg || nseg > (uint32_t)kMaxSeg) {
+    printf("ZG seam_event bad: blk %d rib %u p %u k %u nseg %u fix %u j %u tr %u S %u E %u\n", (int)blockIdx.x, rib, x.p,
+           k, nseg, fix, j, tr, x.S, x.E);
+    R.evc = kNever;
+    return;
+  }
+#endif
+  if (!fix) {
+    const uint32_t side = j == k ? 1u : 0u;            // at C_k: segment k's start; at C_{k+1}: its end side
+    dumps[seam_index(x.p, j, side) + l] = make_uint2(M0, M1);
+    if (side == 1u && k + 1u < nseg) {
+      x.kn = (x.kn & 0xFFFFFu) | ((k + 1u) << 20);
+      R.evc = seg_start(x.E, nseg, k + 1u) + kSegCmp - x.S;
+    } else {
+      R.evc = kNever;
+    }
+  } else {
+    const uint2 b = dumps[seam_index(x.p, j, 1u) + l];
+    const bool ne = (((M0 ^ b.x) | (M1 ^ b.y)) & 0xFE00FE00u) != 0u;
+    const uint64_t bad = __builtin_amdgcn_ballot_w64(ne);
+    if (((bad >> (__lane_id() & 48u)) & 0xFFFFu) == 0u) {   // the row's 64 H bytes agree
+      R.cols = min(R.cols, seg_start(x.E, nseg, j) + kSegWarm + 30u - x.S);
+      x.kn |= 1u << 17;
+      R.evc = kNever;
+    } else if (j + 1u < nseg) {
+      x.kn = (x.kn & 0xFFFFFu) | ((j + 1u) << 20);
+      R.evc = seg_start(x.E, nseg, j + 1u) + kSegCmp - x.S;
+    } else {
+      R.evc = kNever;
+    }
+  }
+  rowx[rib] = x;
 }
 __device__ __forceinline__ uint32_t wave_min_rows(uint32_t v) {
   const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 0), b = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
@@ -423,6 +559,13 @@ __device__ __forceinline__ void traceback(bool due, uint32_t M0, uint32_t M1, ui
   const uint32_t nlf = (C0f - chf) >> 3;
   uint8_t* op = out + ooff + ((c_hi - 14u) >> 3);      // output byte of block c_hi, newest first
   auto prevS = [](uint32_t x) { return x == 0u ? span - (uint32_t)kSlotBytes : x - (uint32_t)kSlotBytes; };
+#ifdef ZRX_GUARD
+  if (walker && ZG_OUT_BAD(op + 1 - (int)nout, op + 1)) {
+    printf("ZG traceback bad: blk %d rib %u T %u cnt %u look %u c_hi %u ooff %u nout %u tr0 %u\n", (int)blockIdx.x, rib, T,
+           cnt, look, c_hi, ooff, nout, tr0);
+    return;
+  }
+#endif
   if (DEFER && uni && nof == 32u && s <= 2u && (nlf == 2u || nlf == 3u)) {   // wave-uniform: every lane
     W->we = (int)nlf;
     W->A = (((C0f - 6u) >> 3) % (uint32_t)kRing) * kSlotBytes;
@@ -506,6 +649,8 @@ struct Packet {
   uint8_t* ring;                                       // this body's first snapshot slot
   uint8_t* ring0;                                      // the block's ring (slot 0)
   Walk* W;                                             // deferred traceback tail (WS >= 0 bodies)
+  RowX* rowx;                                          // the block's cold row facts (seam events)
+  uint2* dumps;                                        // seam dumps
 
   template <int J>
   static __device__ __forceinline__ uint32_t bcast(uint32_t Pa, uint32_t Pb) {   // P word of body column J
@@ -574,6 +719,9 @@ struct Packet {
       if constexpr (CHECKED) {
         const uint32_t tr = tr0 + c;
         if (tr >= s_next) {
+          // seam events sit on body ends (seam columns are multiples of 24 from the row's start)
+          if constexpr (c == 24)
+            if (R.live && tr == R.evc) seam_event(R, tr, M0, M1, l, rib, rowx, dumps);
           events(R, tr, M0, M1);
           s_next = wave_min_rows(R.next);
         }
@@ -601,18 +749,16 @@ __device__ __forceinline__ uint32_t soft_off(uint32_t j) {
 
 template <int CR, int DBG>
 __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64_t so, uint32_t n, Row& R, const Consts& K, uint32_t l,
-                         uint32_t rib, uint8_t* ring_block, uint8_t* __restrict__ out, uint32_t ooff) {
+                         uint32_t rib, uint8_t* ring_block, uint8_t* __restrict__ out, uint32_t ooff,
+                         uint32_t M0, uint32_t M1, RowX* rowx, uint2* __restrict__ dumps) {
   using RT = Rate<CR>;
-  const uint32_t p0 = pos_of(l, 0, 0), p1 = pos_of(l, 0, 1), p2 = pos_of(l, 1, 0), p3 = pos_of(l, 1, 1);
-  uint32_t M0 = ((p1 ? 48u : 0u) << 24) | ((p0 ? 48u : 0u) << 8);   // ALL_INIT0 (viterbilut.h:74-82)
-  uint32_t M1 = ((p3 ? 48u : 0u) << 24) | ((p2 ? 48u : 0u) << 8);
   Walk W;
   W.we = 0;
   W.A = 0;
   W.ix = W.b = W.acc = 0;
   W.voff = 0x80000000u;
   W.ob = (uint64_t)(uintptr_t)out;
-  Packet<CR, DBG> pk{K, R, l, rib, ring_block, ring_block, &W};
+  Packet<CR, DBG> pk{K, R, l, rib, ring_block, ring_block, &W, rowx, dumps};
   // this lane builds the P words of body columns j1 = l and j2 = 16 + l (l < 8)
   const uint32_t j1 = l, j2 = 16u + (l & 7u);
   const uint32_t o1 = soft_off<CR>(j1), o2 = soft_off<CR>(j2);
@@ -711,123 +857,238 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
 }  // namespace v3
 
 // vparams[4p..] = {frame_len, code_rate, soft_len, *}; out_bits[p] = bits written.
-// Requires depth 256 (the only depth the WiFi RX uses: Viterbi.blk:34).  Four packets per
-// wave (16 lanes each); rows of a wave may have different rates and lengths (a wave runs one
-// pass per rate present), so mixed batches are first ordered by k_vit_order.  order may be
-// null (identity).
-template <int DBG>
-__global__ __launch_bounds__(256, 4) void k_viterbi3(const uint8_t* __restrict__ soft, const int64_t* __restrict__ soft_off,
-                                                  const int32_t* __restrict__ vparams, int npkts,
-                                                  uint8_t* __restrict__ out, const int64_t* __restrict__ out_off,
-                                                  int32_t* __restrict__ out_bits, const int32_t* __restrict__ order) {
-  __shared__ uint8_t ring[v3::kRing * v3::kSlotBytes];
+// Requires depth 256 (the only depth the WiFi RX uses: Viterbi.blk:34).  Four rows per wave
+// (16 lanes each); rows of a wave may have different rates and lengths (a wave runs one pass
+// per rate present), so batches are first planned by k_pkt_plan.
+//   rows:  the plan's row table, {packet, k | nseg << 8} per slot, *nrows_p of them (a row is
+//          segment k of nseg of its packet); null: slot = packet, whole frames (nslots).
+//   fix:   the seam pass after a planned launch: slot = packet (segs[p] = its nseg); a row
+//          re-decodes from the first seam whose two dumps disagree (usually none).
+// The grid may be smaller than the rows (block-stride loop).
+template <int DBG, bool FIX>
+__device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, uint32_t ncu, uint32_t ncu_rcp,
+                                             const v3::Consts& K, uint8_t* ring, v3::RowX* rowx,
+                                             const uint8_t* __restrict__ soft, const int64_t* __restrict__ soft_off,
+                                             const int32_t* __restrict__ vparams, uint8_t* __restrict__ out,
+                                             const int64_t* __restrict__ out_off, int32_t* __restrict__ out_bits,
+                                             const int2* __restrict__ rows, const uint8_t* __restrict__ segs,
+                                             uint2* __restrict__ dumps, int32_t* __restrict__ stats) {
+  constexpr int fix = FIX;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t l = lane & 15u;
-  const uint32_t rib = threadIdx.x >> 4;               // row (packet) in block
-  const int slot_p = blockIdx.x * v3::kRows + (int)rib;   // row slot; order[] maps it to a packet
-  const bool valid = slot_p < npkts;
-  const int p = valid && order ? order[slot_p] : slot_p;
-  int fl = 0, cr = 0, n = 0;
-  int64_t so = 0, oo = 0;
-  if (valid) {
-    const int32_t* vp = vparams + 4 * (int64_t)p;
-    fl = vp[0]; cr = vp[1]; n = vp[2];
-    so = soft_off[p]; oo = out_off[p];
-  }
-  const uint32_t cols = valid && n > 0 && cr >= 0 && cr <= 2 ? (uint32_t)(n / (cr == 0 ? 2 : cr == 1 ? 3 : 4)) * (uint32_t)(cr + 1) : 0u;
-  v3::Consts K;
-  v3::make_consts(K, l, rib);
-  // output bytes are addressed as out + 32-bit offset (one uniform base for the whole wave)
-  uint8_t* obase = out + (oo & ~(int64_t)0xFFFFFFFF);
-  const uint32_t ooff = (uint32_t)(oo & 0xFFFFFFFF);
-  uint32_t nbytes = 0;
-  // rows of one rate run together; other rows of the wave sit out that pass.  The row state
-  // is built per pass (not kept across passes), which keeps it out of the register budget.
-  for (int rate = 0; rate < 3; rate++) {
-    const bool mine = cols > 0 && cr == rate;
-    if (__builtin_amdgcn_ballot_w64(mine) == 0) continue;
-    // The soft values of a pass's rows are read through one 32-bit buffer window (run_rows);
-    // rows further apart than that run one at a time (correct, 4x the time; only batches
-    // with more than 4 GiB of soft values can get there).
-    const int64_t lo_me = mine ? so : INT64_MAX, hi_me = mine ? so + (int64_t)max(n, 0) : INT64_MIN;
-    const int64_t lo_w = min(min(v3::rl64(lo_me, 0), v3::rl64(lo_me, 16)), min(v3::rl64(lo_me, 32), v3::rl64(lo_me, 48)));
-    const int64_t hi_w = max(max(v3::rl64(hi_me, 0), v3::rl64(hi_me, 16)), max(v3::rl64(hi_me, 32), v3::rl64(hi_me, 48)));
-    const int passes = hi_w - lo_w > v3::kSoftWindow ? 4 : 1;
-    for (int q = 0; q < passes; q++) {
-      const bool mq = mine && (passes == 1 || (int)(rib & 3u) == q);
-      if (__builtin_amdgcn_ballot_w64(mq) == 0) continue;
-      v3::Row Rr;
-      Rr.ob = 0; Rr.end = (uint32_t)fl * 8u + 6u; Rr.cols = cols;
-      Rr.live = mq;
-      Rr.ppend = Rr.fpend = false;
-      Rr.pT = Rr.plook = Rr.fT = Rr.fcnt = Rr.flook = 0;
-      Rr.pM0 = Rr.pM1 = Rr.fM0 = Rr.fM1 = 0;
-      Rr.nbytes = 0;
-      Rr.next = v3::row_next(Rr);
-      if (rate == 0) v3::run_rows<0, DBG>(soft, so, (uint32_t)max(n, 0), Rr, K, l, rib, ring, obase, ooff);
-      else if (rate == 1) v3::run_rows<1, DBG>(soft, so, (uint32_t)max(n, 0), Rr, K, l, rib, ring, obase, ooff);
-      else v3::run_rows<2, DBG>(soft, so, (uint32_t)max(n, 0), Rr, K, l, rib, ring, obase, ooff);
-      if (mq) nbytes = Rr.nbytes;
+  const uint32_t rib = threadIdx.x >> 4;               // row in block
+  {
+    const int slot = g0 + (int)rib;
+    const bool valid = slot < nrows;
+    int p = slot;
+    uint32_t k = 0, nseg = 1;
+    if (valid && rows) {
+      if (uni) {                                       // a uniform batch: row r = segment r mod u of packet r / u
+        const uint32_t r = v3::order_place((uint32_t)slot, (uint32_t)nrows >> 4, ncu, ncu_rcp);
+        p = (int)v3::udiv_small(r, uni); k = r - (uint32_t)p * uni; nseg = uni;
+      } else {
+        const int2 r = rows[slot];
+        p = r.x; k = (uint32_t)r.y & 0xFFu; nseg = ((uint32_t)r.y >> 8) & 0xFFu;
+      }
+    }
+#ifdef ZRX_GUARD
+    if (valid && ((uint32_t)p >= v3::g_zg_np || nseg == 0 || nseg > (uint32_t)v3::kMaxSeg || k >= nseg)) {
+      printf("ZG row bad: blk %d rib %u slot %d p %d k %u nseg %u fix %d\n", (int)blockIdx.x, rib, slot, p, k, nseg, fix);
+      return;
+    }
+#endif
+    if (valid && fix) nseg = uni ? uni : segs[p];
+#ifdef ZRX_GUARD
+    if (valid && fix && nseg > (uint32_t)v3::kMaxSeg) {
+      printf("ZG segs bad: p %d nseg %u\n", p, nseg);
+      nseg = 1;
+    }
+#endif
+    const bool load = valid && (!fix || nseg > 1u);
+    int fl = 0, cr = 0, n = 0;
+    int64_t so = 0, oo = 0;
+    if (load) {
+      const int32_t* vp = vparams + 4 * (int64_t)p;
+      fl = vp[0]; cr = vp[1]; n = vp[2];
+      so = soft_off[p]; oo = out_off[p];
+    }
+    const uint32_t cols = load && n > 0 && cr >= 0 && cr <= 2 ? (uint32_t)(n / (cr == 0 ? 2 : cr == 1 ? 3 : 4)) * (uint32_t)(cr + 1) : 0u;
+    const uint32_t E = (uint32_t)fl * 8u + 6u;
+    // this row's segment: first column S, last column, seam j of its first seam event
+    uint32_t S = 0, stop = cols, j = 0;
+    bool work = cols > 0;
+    if constexpr (FIX) {
+      // The first (ks) and last (kl) seams whose sides disagree: the fix row starts at ks
+      // from segment ks - 1's state and may stop only at a later seam past kl whose start
+      // state it reproduces (every segment after that one then starts right).
+      uint32_t ks = 0, kl = 0;
+      for (uint32_t jj = 1; __builtin_amdgcn_ballot_w64(work && jj < nseg) != 0; jj++) {
+        bool ne = false;
+        if (work && jj < nseg) {
+          const uint2 a = dumps[v3::seam_index((uint32_t)p, jj, 0) + l], b = dumps[v3::seam_index((uint32_t)p, jj, 1) + l];
+          ne = (((a.x ^ b.x) | (a.y ^ b.y)) & 0xFE00FE00u) != 0u;
+        }
+        const uint64_t bad = __builtin_amdgcn_ballot_w64(ne);
+        if (((bad >> (lane & 48u)) & 0xFFFFu) != 0u) {
+          if (ks == 0u) ks = jj;
+          kl = jj;
+        }
+      }
+      work = work && ks != 0u;
+      if (work) { S = v3::seg_start(E, nseg, ks) + v3::kSegCmp; j = kl + 1u; k = ks; }
+#ifdef ZRX_GUARD
+      if (work && l == 0)
+        printf("ZG fix row: blk %d rib %u p %d nseg %u ks %u S %u E %u cols %u cr %d n %d\n", (int)blockIdx.x, rib, p, nseg,
+               ks, S, E, cols, cr, n);
+#endif
+      if (work && l == 0 && stats) atomicAdd(stats + 1, 1);
+    } else if (nseg > 1u && work) {
+      S = v3::seg_start(E, nseg, k);
+      stop = v3::seg_stop(E, cols, nseg, k);
+      j = k ? k : 1u;
+    }
+    // (cold facts in LDS: read back where needed instead of held in registers by the decode)
+    // (fix rows: k holds ks, the seam they start at)
+    rowx[rib] = v3::RowX{(uint32_t)p, k | (nseg << 8) | ((uint32_t)(fix != 0) << 16) | (j << 20), S, E};
+    const int64_t sS = work ? (int64_t)(S / (uint32_t)(cr + 1)) * (cr == 0 ? 2 : cr == 1 ? 3 : 4) : 0;   // soft values before S
+    so += sS;
+    const uint32_t nS = work ? (uint32_t)((int64_t)n - sS) : 0u;
+    const uint32_t colsS = work ? min(cols, stop) - S : 0u;
+    oo += S >> 3;
+    // output bytes are addressed as out + 32-bit offset (one uniform base for the whole wave)
+    uint8_t* obase = out + (oo & ~(int64_t)0xFFFFFFFF);
+    const uint32_t ooff = (uint32_t)(oo & 0xFFFFFFFF);
+    uint32_t nbytes = 0;
+    // rows of one rate run together; other rows of the wave sit out that pass.  The row state
+    // is built per pass (not kept across passes), which keeps it out of the register budget.
+    for (int rate = 0; rate < 3; rate++) {
+      const bool mine = work && cr == rate;
+      if (__builtin_amdgcn_ballot_w64(mine) == 0) continue;
+      // The soft values of a pass's rows are read through one 32-bit buffer window (run_rows);
+      // rows further apart than that run one at a time (correct, 4x the time; only batches
+      // with more than 4 GiB of soft values can get there).
+      const int64_t lo_me = mine ? so : INT64_MAX, hi_me = mine ? so + (int64_t)nS : INT64_MIN;
+      const int64_t lo_w = min(min(v3::rl64(lo_me, 0), v3::rl64(lo_me, 16)), min(v3::rl64(lo_me, 32), v3::rl64(lo_me, 48)));
+      const int64_t hi_w = max(max(v3::rl64(hi_me, 0), v3::rl64(hi_me, 16)), max(v3::rl64(hi_me, 32), v3::rl64(hi_me, 48)));
+      const int passes = hi_w - lo_w > v3::kSoftWindow ? 4 : 1;
+      for (int q = 0; q < passes; q++) {
+        const bool mq = mine && (passes == 1 || (int)(rib & 3u) == q);
+        if (__builtin_amdgcn_ballot_w64(mq) == 0) continue;
+        // start state, output base and first seam event of the row (v3::seg_start)
+        const v3::RowX x = rowx[rib];
+        const uint32_t xk = x.kn & 0xFFu, xn = (x.kn >> 8) & 0xFFu, xj = x.kn >> 20;
+        const bool xfix = (x.kn >> 16) & 1u;
+        uint32_t M0, M1;
+        if (xfix && mq) {                               // segment ks - 1's exact state at S = C_ks
+          const uint2 a = dumps[v3::seam_index(x.p, x.kn & 0xFFu, 0) + l];
+          M0 = a.x; M1 = a.y;
+        } else if (xk) {                                // warm-up from zero
+          M0 = M1 = 0u;
+        } else {                                        // ALL_INIT0 (viterbilut.h:74-82)
+          const uint32_t p0 = v3::pos_of(l, 0, 0), p1 = v3::pos_of(l, 0, 1), p2 = v3::pos_of(l, 1, 0), p3 = v3::pos_of(l, 1, 1);
+          M0 = ((p1 ? 48u : 0u) << 24) | ((p0 ? 48u : 0u) << 8);
+          M1 = ((p3 ? 48u : 0u) << 24) | ((p2 ? 48u : 0u) << 8);
+        }
+        v3::Row Rr;
+        Rr.ob = xfix ? v3::kSegWarm - v3::kSegCmp : xk ? v3::kSegWarm : 0u;
+        Rr.end = x.E - x.S; Rr.cols = colsS;
+        Rr.evc = xj != 0u && xj < xn ? v3::seg_start(x.E, xn, xj) + v3::kSegCmp - x.S : v3::kNever;
+        Rr.live = mq;
+        Rr.ppend = Rr.fpend = false;
+        Rr.pT = Rr.plook = Rr.fT = Rr.fcnt = Rr.flook = 0;
+        Rr.pM0 = Rr.pM1 = Rr.fM0 = Rr.fM1 = 0;
+        Rr.nbytes = 0;
+        Rr.next = v3::row_next(Rr);
+        if (rate == 0) v3::run_rows<0, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M0, M1, rowx, dumps);
+        else if (rate == 1) v3::run_rows<1, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M0, M1, rowx, dumps);
+        else v3::run_rows<2, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M0, M1, rowx, dumps);
+        if (mq) nbytes = Rr.nbytes;
+      }
+    }
+    // the frame's bit count: from its last segment, or from a fix row that ran to the end
+    if (valid && l == 0) {
+      const v3::RowX x = rowx[rib];
+      const uint32_t xk = x.kn & 0xFFu, xn = (x.kn >> 8) & 0xFFu;
+      const bool last = (x.kn >> 16) & 1u ? work && ((x.kn >> 17) & 1u) == 0u : xk + 1u == xn;
+      if (last) out_bits[x.p] = nbytes == 0xFFFFFFFFu ? -1 : (int32_t)((nbytes + (x.S >> 3)) * 8u);
     }
   }
-  if (valid && l == 0) out_bits[p] = nbytes == 0xFFFFFFFFu ? -1 : (int32_t)(nbytes * 8u);
+}
+template <int DBG, bool FIX = false>
+__global__ __launch_bounds__(256, 4) void k_viterbi3(const uint8_t* __restrict__ soft, const int64_t* __restrict__ soft_off,
+                                                  const int32_t* __restrict__ vparams, int nslots,
+                                                  uint8_t* __restrict__ out, const int64_t* __restrict__ out_off,
+                                                  int32_t* __restrict__ out_bits, const int2* __restrict__ rows,
+                                                  int32_t* __restrict__ nrows_p, const uint8_t* __restrict__ segs,
+                                                  uint2* __restrict__ dumps) {
+  __shared__ uint8_t ring[v3::kRing * v3::kSlotBytes];
+  __shared__ v3::RowX rowx[v3::kRows];
+  // the plan header (v3::PlanWord): rows, the fix pass's count of re-decoded rows, the
+  // segments per packet of a uniform batch (0: row table), the CU count of the placement
+  const int nrows = FIX || !nrows_p ? nslots : nrows_p[v3::kPlanRows];
+  const uint32_t uni = nrows_p ? (uint32_t)nrows_p[v3::kPlanUniform] : 0u;
+  const uint32_t ncu = nrows_p ? max((uint32_t)nrows_p[v3::kPlanNcu], 2u) : 2u;
+  const uint32_t ncu_rcp = 0xFFFFFFFFu / ncu + 1u;
+  v3::Consts K;
+  v3::make_consts(K, threadIdx.x & 15u, threadIdx.x >> 4);
+  if constexpr (FIX) {                                 // block-stride over the packets
+    for (int g0 = blockIdx.x * v3::kRows; g0 < nrows; g0 += gridDim.x * v3::kRows)
+      viterbi_rows<DBG, true>(g0, nrows, uni, ncu, ncu_rcp, K, ring, rowx, soft, soft_off, vparams, out, out_off, out_bits, rows, segs, dumps,
+                              nrows_p);
+  } else {
+    const int g0 = blockIdx.x * v3::kRows;
+    if (g0 < nrows)
+      viterbi_rows<DBG, false>(g0, nrows, uni, ncu, ncu_rcp, K, ring, rowx, soft, soft_off, vparams, out, out_off, out_bits, rows, segs,
+                               dumps, nullptr);
+  }
 }
 
-// Packet order for k_viterbi3 over a mixed batch (BASELINE config 5): by code rate, then by
-// trellis length, longest first, so the four rows of a wave share one rate and similar
-// lengths.  One 1024-thread block; counting sort over (rate, 24-column bodies) keys.  Packets
-// are read coalesced (p = 1024 k + thread, 16 loads per thread in flight) and their keys
-// recomputed in the scatter pass, so
-// any batch size is ordered; a wave whose 64 packets share a key (any uniform batch) counts
-// and places them with one LDS atomic.  1024 length buckets cover 24576 columns, i.e. every
-// 802.11a frame (at most 8 x 2050 + 6 = 16406 columns); longer device-API frames share the
-// last bucket.  Within a bucket the order is whatever the atomics give (each packet decodes
-// the same wherever it lands).
+// Row order for k_viterbi3 (k_pkt_plan): by code rate, then by trellis length of the row
+// (a frame or one of its segments), longest first, so the four rows of a wave share one rate
+// and similar lengths.  Counting sort over (rate, 24-column bodies) keys; 1024 length buckets
+// cover 24576 columns, i.e. every 802.11a frame (at most 8 x 2050 + 6 = 16406 columns);
+// longer device-API frames share the last bucket.  Within a bucket the order is whatever the
+// atomics give (each row decodes the same wherever it lands).
 constexpr int kOrderLen = 1024;                        // length buckets of 24 columns
 constexpr int kOrderKeys = 3 * kOrderLen + 1;          // + one bucket for packets with no work
 constexpr int kOrderPerThread = (kOrderKeys + 1023) / 1024;
-__device__ __forceinline__ uint32_t order_key_of(int cr, int n) {
-  if (n <= 0 || cr < 0 || cr > 2) return 3u * kOrderLen;
-  const uint32_t u = (uint32_t)n;                      // trellis columns, with constant divisors
-  const uint32_t cols = cr == 0 ? u >> 1 : cr == 1 ? (u / 3u) * 2u : (u >> 2) * 3u;
-  const uint32_t bodies = min((cols + 23u) / 24u, (uint32_t)kOrderLen - 1u);
+__device__ __forceinline__ uint32_t order_key_len(int cr, uint32_t len) {
+  if (len == 0 || cr < 0 || cr > 2) return 3u * kOrderLen;
+  const uint32_t bodies = min((len + 23u) / 24u, (uint32_t)kOrderLen - 1u);
   return (uint32_t)cr * kOrderLen + (kOrderLen - 1u - bodies);
 }
-__device__ __forceinline__ uint32_t order_key(const int32_t* __restrict__ vparams, int p) {
-  const int32_t* vp = vparams + 4 * (int64_t)p;
-  return order_key_of(vp[1], vp[2]);
-}
-// Sorted position -> row slot: the nfull whole blocks of 16 rows placed "snake" over ncu
-// CUs: in odd rounds of ncu blocks the order is reversed, so with blocks dealt to CU
-// (slot mod ncu) — what the dispatcher does when every block of the launch is resident
-// (scripts/ubench/hwid.hip) — the CU running one of the longest blocks gets one of the
-// shortest of the next round beside it.  An involution within each round; a partial last
-// block stays in place.
-__device__ __forceinline__ uint32_t order_place(uint32_t pos, uint32_t nfull, uint32_t ncu) {
-  const uint32_t b = pos >> 4;
-  if (b >= nfull) return pos;
-  const uint32_t r = b / ncu, c = b - r * ncu, base = r * ncu;
-  const uint32_t m = min(ncu, nfull - base);
-  return ((r & 1u) ? base + m - 1u - c : b) * 16u + (pos & 15u);
+// trellis columns of a packet's soft input (constant divisors)
+__device__ __forceinline__ uint32_t cols_of(int cr, int n) {
+  if (n <= 0 || cr < 0 || cr > 2) return 0u;
+  const uint32_t u = (uint32_t)n;
+  return cr == 0 ? u >> 1 : cr == 1 ? (u / 3u) * 2u : (u >> 2) * 3u;
 }
 // Adds this wave's valid lanes to hist[key] and returns each lane's slot (old count + rank
-// among the lanes sharing its key): one atomic when the wave's keys agree.
+// among the lanes sharing its key).  The lanes of the wave's first two keys are counted with
+// one atomic each (a uniform batch has one key, the segments of a mixed one few), the rest
+// one atomic per lane, so lanes sharing a key do not serialize on one LDS address.
 __device__ __forceinline__ uint32_t order_claim(uint32_t* hist, bool valid, uint32_t key) {
-  const uint64_t mask = __builtin_amdgcn_ballot_w64(valid);
-  if (mask == 0) return 0;
-  const uint32_t first = (uint32_t)__builtin_ctzll(mask);
-  const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)first);
-  if (__builtin_amdgcn_ballot_w64(valid && key == k0) == mask) {
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+  uint64_t rem = __builtin_amdgcn_ballot_w64(valid);
+  uint32_t slot = 0;
+  const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+  for (int it = 0; it < 2; it++) {
+    if (rem == 0) return slot;
+    const uint32_t first = (uint32_t)__builtin_ctzll(rem);
+    const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)first);
+    const uint64_t m = __builtin_amdgcn_ballot_w64(valid && key == k0);
     uint32_t base = 0;
-    if ((threadIdx.x & 63u) == first) base = atomicAdd(&hist[k0], (uint32_t)__builtin_popcountll(mask));
-    return (uint32_t)__builtin_amdgcn_readlane((int)base, (int)first) + rank;
+    if (lane == first) base = atomicAdd(&hist[k0], (uint32_t)__builtin_popcountll(m));
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)first);
+    if ((m >> lane) & 1u) slot = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    rem &= ~m;
   }
-  return valid ? atomicAdd(&hist[key], 1u) : 0u;
+  if ((rem >> lane) & 1u) slot = atomicAdd(&hist[key], 1u);
+  return slot;
 }
-// hist[] counts -> exclusive starts (1024 threads, kOrderPerThread buckets each); the caller
-// syncs before and after.
-__device__ __forceinline__ void order_hist_scan(uint32_t* hist) {
+// hist[] counts -> exclusive starts (1024 threads, kOrderPerThread buckets each); returns the
+// total.  The caller syncs before and after.
+__device__ __forceinline__ uint32_t order_hist_scan(uint32_t* hist) {
   __shared__ uint32_t wsum[16];
   const int t = threadIdx.x;
   uint32_t v[kOrderPerThread], mine = 0;
@@ -841,40 +1102,13 @@ __device__ __forceinline__ void order_hist_scan(uint32_t* hist) {
   }
   if ((t & 63) == 63) wsum[t >> 6] = inc;
   __syncthreads();
-  uint32_t ex = inc - mine;
+  uint32_t ex = inc - mine, total = 0;
   for (int w = 0; w < (t >> 6); w++) ex += wsum[w];
+  for (int w = 0; w < 16; w++) total += wsum[w];
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < kOrderPerThread; j++) { hist[kOrderPerThread * t + j] = ex; ex += v[j]; }
-}
-__global__ __launch_bounds__(1024) void k_vit_order(const int32_t* __restrict__ vparams, int npkts,
-                                                    int32_t* __restrict__ order, int ncu) {
-  __shared__ uint32_t hist[kOrderPerThread * 1024];
-  const int t = threadIdx.x;
-  for (int i = t; i < kOrderPerThread * 1024; i += blockDim.x) hist[i] = 0;
-  __syncthreads();
-  constexpr int kPer = 16;                             // keys per thread in flight together
-  for (int b = 0; b < npkts; b += 1024 * kPer) {
-    uint32_t key[kPer];
-#pragma unroll
-    for (int i = 0; i < kPer; i++) key[i] = b + 1024 * i + t < npkts ? order_key(vparams, b + 1024 * i + t) : 0u;
-#pragma unroll
-    for (int i = 0; i < kPer; i++) order_claim(hist, b + 1024 * i + t < npkts, key[i]);
-  }
-  __syncthreads();
-  order_hist_scan(hist);
-  __syncthreads();
-  for (int b = 0; b < npkts; b += 1024 * kPer) {
-    uint32_t key[kPer];
-#pragma unroll
-    for (int i = 0; i < kPer; i++) key[i] = b + 1024 * i + t < npkts ? order_key(vparams, b + 1024 * i + t) : 0u;
-#pragma unroll
-    for (int i = 0; i < kPer; i++) {
-      const int p = b + 1024 * i + t;
-      const uint32_t slot = order_claim(hist, p < npkts, key[i]);
-      if (p < npkts) order[order_place(slot, (uint32_t)npkts >> 4, (uint32_t)ncu)] = p;
-    }
-  }
+  return total;
 }
 
 }  // namespace zrx

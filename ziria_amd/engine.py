@@ -57,6 +57,12 @@ class RxEngine:
         check(lib().zrx_get_timing(self._h, ms), "zrx_get_timing")
         return dict(zip(STAGES, [float(v) for v in ms]))
 
+    def plan_stats(self):
+        """(decoder rows, frames re-decoded by the seam pass) of the last Viterbi launch."""
+        st = (C.c_int32 * 2)()
+        check(lib().zrx_plan_stats(self._h, st), "zrx_plan_stats")
+        return int(st[0]), int(st[1])
+
     # ------------------------------------------------------------------ launches
     def fft64(self, sym, out=None):
         """sym: int16 [S, 64, 2] on the device -> FFT64 of every symbol."""
