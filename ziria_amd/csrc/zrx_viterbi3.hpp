@@ -1029,6 +1029,7 @@ __global__ __launch_bounds__(256, 4) void k_viterbi3(const uint8_t* __restrict__
   const uint32_t uni = nrows_p ? (uint32_t)nrows_p[v3::kPlanUniform] : 0u;
   const uint32_t ncu = nrows_p ? max((uint32_t)nrows_p[v3::kPlanNcu], 2u) : 2u;
   const uint32_t ncu_rcp = 0xFFFFFFFFu / ncu + 1u;
+  if (FIX && uni == 1u) return;                        // a uniform batch of whole frames has no seams
   v3::Consts K;
   v3::make_consts(K, threadIdx.x & 15u, threadIdx.x >> 4);
   if constexpr (FIX) {                                 // block-stride over the packets
