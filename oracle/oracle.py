@@ -75,6 +75,23 @@ def fft64(x):
     return out.reshape(x.shape)
 
 
+FFT_SIZES = (12, 16, 24, 32, 36, 48, 60, 64, 72, 96, 108, 120, 128, 144, 180, 192, 216, 240, 256, 288, 300,
+             324, 360, 384, 432, 480, 512, 540, 576, 600, 648, 720, 768, 864, 900, 960, 972, 1024, 1080, 1152,
+             1200, 2048)                       # __ext_sora_fft's sizes (csrc/sora_ext_lib.cpp:2672-2812)
+
+
+def fft_n(n, x):
+    """FFTSafe<n> of every row: x int16 [..., n, 2].  Raises for a size the reference rejects."""
+    x = np.ascontiguousarray(x, dtype=np.int16)
+    flat = x.reshape(-1, n, 2)
+    out = np.empty_like(flat)
+    L = lib()
+    for i in range(flat.shape[0]):
+        if L.zo_fft_n(int(n), _p(flat[i]), _p(out[i])) != 0:
+            raise ValueError(f"fft size {n} not supported")
+    return out.reshape(x.shape)
+
+
 def v_shift_right_complex16(x, shift):
     x = np.ascontiguousarray(x, dtype=np.int16).reshape(-1, 2)
     z = np.zeros_like(x)

@@ -87,6 +87,121 @@ void zo_fft64(const zo_c16* in, zo_c16* out) {
   for (int i = 0; i < 64; i++) out[i] = x[bitrev6(i)];
 }
 
+/* ---- FFTSafe<N> for every size __ext_sora_fft dispatches (csrc/sora_ext_lib.cpp:2672-2812) */
+static inline zo_c16 cshr3(zo_c16 a) { zo_c16 r = {(int16_t)(a.re >> 3), (int16_t)(a.im >> 3)}; return r; }
+static inline zo_c16 cinv(zo_c16 a) { zo_c16 r = {inv16(a.re), inv16(a.im)}; return r; }
+static inline zo_c16 tw(int N, int k, int n) { zo_c16 t; zo_twiddle(N, k, n, &t.re, &t.im); return t; }
+static inline zo_c16 mul_c(zo_c16 a, zo_c16 b) { return mul_shift(a, b.re, b.im); }
+
+/* FFTSSE_3<N>: csrc/sora_ext_lib_fft.hpp:111-171 (radix-3 DIF stage, input >> 2, the
+   rotations e^{-j2pi/3}, e^{-j4pi/3} as (-16384, -+28378), outputs in natural thirds) */
+static void fft_stage3(zo_c16* x, int N) {
+  const zo_c16 k1 = {-16384, -28378}, k2 = {-16384, 28378};
+  const int M = N / 3;
+  for (int n = 0; n < M; n++) {
+    zo_c16 a = cshr2(x[n]), b = cshr2(x[n + M]), c = cshr2(x[n + 2 * M]);
+    zo_c16 bk1 = mul_c(b, k1), bk2 = mul_c(b, k2), ck1 = mul_c(c, k1), ck2 = mul_c(c, k2);
+    x[n] = cadd(cadd(a, b), c);
+    x[n + M] = mul_c(cadd(cadd(a, bk1), ck2), tw(N, 1, n));
+    x[n + 2 * M] = mul_c(cadd(cadd(a, bk2), ck1), tw(N, 2, n));
+  }
+}
+/* FFTSSE_5<N>: csrc/sora_ext_lib_fft.hpp:253-349 (radix-5 DIF stage, input >> 3) */
+static void fft_stage5(zo_c16* x, int N) {
+  const zo_c16 k1 = {10126, -31164}, k2 = {-26510, -19261}, k3 = {-26510, 19261}, k4 = {10126, 31164};
+  const int M = N / 5;
+  for (int n = 0; n < M; n++) {
+    zo_c16 a = cshr3(x[n]), b = cshr3(x[n + M]), c = cshr3(x[n + 2 * M]), d = cshr3(x[n + 3 * M]),
+           e = cshr3(x[n + 4 * M]);
+    zo_c16 bk1 = mul_c(b, k1), bk2 = mul_c(b, k2), bk3 = mul_c(b, k3), bk4 = mul_c(b, k4);
+    zo_c16 ck1 = mul_c(c, k1), ck2 = mul_c(c, k2), ck3 = mul_c(c, k3), ck4 = mul_c(c, k4);
+    zo_c16 dk1 = mul_c(d, k1), dk2 = mul_c(d, k2), dk3 = mul_c(d, k3), dk4 = mul_c(d, k4);
+    zo_c16 ek1 = mul_c(e, k1), ek2 = mul_c(e, k2), ek3 = mul_c(e, k3), ek4 = mul_c(e, k4);
+    x[n] = cadd(cadd(cadd(a, b), cadd(c, d)), e);
+    x[n + M] = mul_c(cadd(cadd(cadd(a, bk1), cadd(ck2, dk3)), ek4), tw(N, 1, n));
+    x[n + 2 * M] = mul_c(cadd(cadd(cadd(a, bk2), cadd(ck4, dk1)), ek3), tw(N, 2, n));
+    x[n + 3 * M] = mul_c(cadd(cadd(cadd(a, bk3), cadd(ck1, dk4)), ek2), tw(N, 3, n));
+    x[n + 4 * M] = mul_c(cadd(cadd(cadd(a, bk4), cadd(ck3, dk2)), ek1), tw(N, 4, n));
+  }
+}
+/* FFTSSEEx<8>: csrc/fft_r4difx.hpp:142-218, the SSE lane sequence restated per complex
+   value: input >> 3; d = x[k] - x[k+4], s = x[k] + x[k+4]; the lower half rotates d2, d3
+   by (im, ~re), combines, multiplies by (32767,0), (23169,-23169), (32767,0),
+   (-23169,-23169) and finishes with XOR-as-negate pairs; the upper half is a 4-point DFT
+   of s with the same pairing.  Output positions 0..3 = the upper half, 4..7 = the lower. */
+static void fft8(zo_c16* x) {
+  zo_c16 d[4], s[4], e[4], f[4], t[4], u[4];
+  for (int k = 0; k < 4; k++) {
+    zo_c16 a = cshr3(x[k]), b = cshr3(x[k + 4]);
+    d[k] = csub(a, b);
+    s[k] = cadd(a, b);
+  }
+  zo_c16 m2 = {d[2].im, inv16(d[2].re)}, m3 = {d[3].im, inv16(d[3].re)};
+  e[0] = cadd(d[0], m2); e[1] = cadd(d[1], m3); e[2] = cadd(cinv(m2), d[0]); e[3] = cadd(cinv(m3), d[1]);
+  const zo_c16 w[4] = {{32767, 0}, {23169, -23169}, {32767, 0}, {-23169, -23169}};
+  for (int k = 0; k < 4; k++) f[k] = mul_c(e[k], w[k]);
+  t[0] = cadd(s[0], s[2]); t[1] = cadd(s[1], s[3]); t[2] = cadd(cinv(s[2]), s[0]); t[3] = cadd(cinv(s[3]), s[1]);
+  u[0] = t[0]; u[1] = t[1]; u[2] = t[2]; u[3].re = t[3].im; u[3].im = inv16(t[3].re);
+  x[0] = cadd(u[0], u[1]); x[1] = cadd(cinv(u[1]), u[0]); x[2] = cadd(u[2], u[3]); x[3] = cadd(cinv(u[3]), u[2]);
+  x[4] = cadd(f[0], f[1]); x[5] = cadd(f[0], cinv(f[1])); x[6] = cadd(f[2], f[3]); x[7] = cadd(f[2], cinv(f[3]));
+}
+/* The radix of the first stage of FFTSSEEx<N>: the template specialisations route these
+   sizes to FFTSSE_3W (csrc/sora_ext_lib_fft.hpp:190-251) and FFTSSE_5W (:366-430); every
+   other size takes the generic radix-4 FFTSSEEx (csrc/fft_r4difx.hpp:99-109); 4 and 8 are
+   the base cases (:111-218). */
+int zo_fft_radix(int N) {
+  switch (N) {
+    case 4: case 8: return 0;
+    case 12: case 24: case 36: case 72: case 108: case 216: case 324: case 648: case 972: return 3;
+    case 60: case 120: case 180: case 300: case 360: case 540: case 600: case 900: case 1080: return 5;
+    default: return 4;
+  }
+}
+static void fft_ex(zo_c16* x, int N) {
+  const int r = zo_fft_radix(N);
+  if (r == 0) { if (N == 4) fft4(x); else fft8(x); return; }
+  if (r == 4) fft_stage(x, N); else if (r == 3) fft_stage3(x, N); else fft_stage5(x, N);
+  for (int q = 0; q < r; q++) fft_ex(x + q * (N / r), N / r);
+}
+/* Frequency index held at each position after fft_ex (the reference's bFFT{N}LUTMap is its
+   inverse, csrc/sora_ext_lib_fft_coeffs.hpp:15053-15260): a radix-4 stage leaves residues
+   0, 2, 1, 3 in its quarters, radix 3 / 5 stages leave them in order, the base cases are
+   bit-reversed. */
+void zo_fft_freq_of_pos(int N, int* idx) {
+  const int r = zo_fft_radix(N);
+  if (r == 0) {
+    for (int p = 0; p < N; p++) idx[p] = N == 4 ? ((p & 1) << 1 | (p >> 1)) : ((p & 1) << 2 | (p & 2) | (p >> 2));
+    return;
+  }
+  const int M = N / r;
+  int* sub = (int*)malloc(sizeof(int) * M);
+  zo_fft_freq_of_pos(M, sub);
+  static const int res4[4] = {0, 2, 1, 3};
+  for (int q = 0; q < r; q++)
+    for (int p = 0; p < M; p++) idx[q * M + p] = r * sub[p] + (r == 4 ? res4[q] : q);
+  free(sub);
+}
+int zo_fft_supported(int N) {
+  static const int sz[] = {16, 32, 64, 128, 256, 512, 1024, 2048, 12, 24, 36, 48, 60, 72, 96, 108, 120, 144,
+                           180, 192, 216, 240, 288, 300, 324, 360, 384, 432, 480, 540, 576, 600, 648, 720, 768,
+                           864, 900, 960, 972, 1080, 1152, 1200};
+  for (unsigned i = 0; i < sizeof(sz) / sizeof(sz[0]); i++) if (sz[i] == N) return 1;
+  return 0;
+}
+/* FFTSafe<N> (csrc/fft_r4difx.hpp:220-237): the stages on a copy, then out[f] = the
+   position holding frequency f.  Returns 0, or -1 for a size the reference rejects. */
+int zo_fft_n(int N, const zo_c16* in, zo_c16* out) {
+  if (!zo_fft_supported(N)) return -1;
+  zo_c16* x = (zo_c16*)malloc(sizeof(zo_c16) * N);
+  int* idx = (int*)malloc(sizeof(int) * N);
+  memcpy(x, in, sizeof(zo_c16) * N);
+  fft_ex(x, N);
+  zo_fft_freq_of_pos(N, idx);
+  for (int p = 0; p < N; p++) out[idx[p]] = x[p];
+  free(x); free(idx);
+  return 0;
+}
+
 /* __ext_v_shift_right_complex16 (csrc/sora_ext_lib.cpp:1979-1995): whole groups of 4
    complex values use _mm_srai_epi16 (arithmetic, counts > 15 fill with the sign); the
    remaining values use unum16 >> shift (logical). */

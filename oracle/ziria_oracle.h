@@ -23,6 +23,11 @@ typedef struct { int16_t re, im; } zo_c16;
 
 /* ---- FFT64: csrc/fft_r4difx.hpp:54-140,220-237, csrc/sora_ext_lib_fft.hpp:41-108 ---- */
 void zo_fft64(const zo_c16* in, zo_c16* out);
+/* FFTSafe<N> for every size __ext_sora_fft dispatches (12..2048); -1 for others */
+int zo_fft_n(int N, const zo_c16* in, zo_c16* out);
+int zo_fft_supported(int N);
+int zo_fft_radix(int N);
+void zo_fft_freq_of_pos(int N, int* idx);
 /* twiddles twFFTLUT{N}_{k} (csrc/sora_ext_lib_fft_coeffs.hpp:53-78,298-359) regenerated */
 void zo_twiddle(int N, int k, int n, int16_t* re, int16_t* im);
 

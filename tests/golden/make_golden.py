@@ -15,7 +15,11 @@ Sources, in order of authority:
      reference (wplc is unavailable), so chain fixtures use the reference FFT + Viterbi
      bricks with the oracle's glue, which is itself pinned by the encdec KATs above.
 
+  4. ref_fftn.npz: the whole tests/libs/test_fft KAT (all 42 sizes of __ext_sora_fft) and
+     the compiled reference FFT brick on random, saturating and small vectors of every size.
+
 Usage: python tests/golden/make_golden.py        (all fixtures)
+       python tests/golden/make_golden.py fftn   (ref_fftn.npz only)
        python tests/golden/make_golden.py eq     (ref_eq.npz only)
        python tests/golden/make_golden.py fe     (ref_fe.npz only)
 """
@@ -315,6 +319,35 @@ def fe_vectors(R):
     return d
 
 
+def fftn_vectors(R, per=6, seed=0xFF7):
+    """test_fft KAT (test_fft.wpl: one block per size, in O.FFT_SIZES order) + reference
+    brick outputs for `per` vectors of every size, concatenated (offsets in vec_off)."""
+    d = {}
+    inp = rd(REF + "/tests/libs/test_fft.infile")
+    gnd = rd(REF + "/tests/libs/test_fft.outfile.ground")
+    tot = sum(O.FFT_SIZES)
+    d["sizes"] = np.array(O.FFT_SIZES, np.int32)
+    d["kat_in"] = inp[: 2 * tot].reshape(tot, 2).astype(np.int16)
+    d["kat_out"] = gnd[: 2 * tot].reshape(tot, 2).astype(np.int16)
+    rng = np.random.default_rng(seed)
+    xs, ys, off = [], [], [0]
+    for n in O.FFT_SIZES:
+        for t in range(per):
+            if t < 2:
+                x = rng.integers(-32768, 32768, (n, 2))
+            elif t < 4:
+                x = rng.choice(np.array([-32768, -32767, 32767, 0, 1, -1]), (n, 2))
+            else:
+                x = rng.integers(-3000, 3000, (n, 2))
+            x = np.ascontiguousarray(x, np.int16)
+            y = np.zeros_like(x)
+            R.zref_sora_fft(ptr(y), n, ptr(x))
+            xs.append(x); ys.append(y); off.append(off[-1] + n)
+    d["vec_in"], d["vec_out"] = np.concatenate(xs), np.concatenate(ys)
+    d["vec_off"], d["vec_per"] = np.array(off, np.int64), np.int32(per)
+    return d
+
+
 def main():
     O.build()
     R = O.ref()
@@ -322,6 +355,10 @@ def main():
     if sys.argv[1:] == ["fe"]:
         np.savez_compressed(os.path.join(HERE, "ref_fe.npz"), **fe_vectors(R))
         print("ref_fe.npz", os.path.getsize(os.path.join(HERE, "ref_fe.npz")))
+        return
+    if sys.argv[1:] == ["fftn"]:
+        np.savez_compressed(os.path.join(HERE, "ref_fftn.npz"), **fftn_vectors(R))
+        print("ref_fftn.npz", os.path.getsize(os.path.join(HERE, "ref_fftn.npz")))
         return
     if sys.argv[1:] == ["eq"]:
         np.savez_compressed(os.path.join(HERE, "ref_eq.npz"), **eq_vectors(R))
@@ -334,6 +371,7 @@ def main():
     np.savez_compressed(os.path.join(HERE, "ref_chain.npz"), **chain_vectors(R))
     np.savez_compressed(os.path.join(HERE, "ref_eq.npz"), **eq_vectors(R))
     np.savez_compressed(os.path.join(HERE, "ref_fe.npz"), **fe_vectors(R))
+    np.savez_compressed(os.path.join(HERE, "ref_fftn.npz"), **fftn_vectors(R))
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

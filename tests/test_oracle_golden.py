@@ -16,6 +16,32 @@ def test_fft64_reference_vectors(oracle, golden):
     assert (oracle.fft64(g["fft_in"]) == g["fft_out"]).all()
 
 
+def test_fft_all_sizes_kat(oracle, golden):
+    """tests/libs/test_fft (one block of every __ext_sora_fft size, 12..2048)."""
+    g = golden["ref_fftn"]
+    off = 0
+    for n in g["sizes"]:
+        n = int(n)
+        assert (oracle.fft_n(n, g["kat_in"][off:off + n]) == g["kat_out"][off:off + n]).all(), n
+        off += n
+
+
+def test_fft_all_sizes_reference_vectors(oracle, golden):
+    """Reference FFT brick outputs on random, saturating and small vectors of every size."""
+    g = golden["ref_fftn"]
+    o, per = g["vec_off"], int(g["vec_per"])
+    for i, n in enumerate(g["sizes"]):
+        for t in range(per):
+            a, b = o[i * per + t], o[i * per + t + 1]
+            assert (oracle.fft_n(int(n), g["vec_in"][a:b]) == g["vec_out"][a:b]).all(), (int(n), t)
+
+
+def test_fft_unsupported_sizes(oracle):
+    for n in (0, 8, 20, 63, 100, 4096):
+        with pytest.raises(ValueError):
+            oracle.fft_n(n, np.zeros((max(n, 1), 2), np.int16))
+
+
 def test_demap_tables(oracle, golden):
     t = golden["ref_tables"]
     L = oracle.luts()

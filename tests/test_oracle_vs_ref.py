@@ -29,6 +29,20 @@ def test_fft_random(oracle, ref):
         assert (oracle.fft64(x) == o).all()
 
 
+def test_fft_all_sizes_random(oracle, ref):
+    """Every __ext_sora_fft size (csrc/sora_ext_lib.cpp:2672-2812), and a rejected size that
+    leaves the output untouched."""
+    rng = np.random.default_rng(321)
+    for n in oracle.FFT_SIZES:
+        for t in range(12):
+            x = rng.integers(-32768, 32768, (n, 2)).astype(np.int16)
+            if t % 3 == 1:
+                x = rng.choice(np.array([-32768, 32767, -1, 0, 1], np.int16), (n, 2))
+            o = np.zeros_like(x)
+            ref.zref_sora_fft(_p(o), n, _p(x))
+            assert (oracle.fft_n(n, x) == o).all(), (n, t)
+
+
 def test_viterbi_luts(oracle, ref):
     ma = np.zeros(1024, np.uint8)
     mb = np.zeros(1024, np.uint8)
