@@ -31,9 +31,10 @@ struct complex16 { int16_t re; int16_t im; };
 /* ================================================================ Part 1: reference bricks */
 
 /* Replaces __ext_sora_fft (reference csrc/sora_ext_lib.cpp:2672-2812, declared
- * lib/externals.blk:201-202).  Size 64 (the 802.11a OFDM symbol) runs on the GPU; any
+ * lib/externals.blk:201-202): FFTSafe<nFFTSize> on the GPU for every size the reference
+ * dispatches (16, 32, ..., 2048 and the LTE sizes 12 .. 1200, listed at zrx_fft_dev); any
  * other size prints the reference's error message and leaves `out` untouched, as the
- * reference does for a size it does not support (:2808-2810). */
+ * reference does (:2808-2810). */
 void __ext_sora_fft(struct complex16* out, int nFFTSize, struct complex16* in, int unused1);
 
 /* Replaces __ext_sora_fft_dynamic (sora_ext_lib.cpp:2816-2820, externals.blk:205-206). */
@@ -152,6 +153,12 @@ int zrx_get_timing(zrx_ctx* ctx, float* ms5);
 
 /* d_in/d_out: 64*nsym complex16 each (may alias). */
 int zrx_fft64_dev(zrx_ctx* ctx, const struct complex16* d_in, struct complex16* d_out, int64_t nsym);
+/* FFTSafe<nfft> (csrc/fft_r4difx.hpp:220-237) of count consecutive blocks of nfft complex16
+ * (d_in/d_out may alias), for every size __ext_sora_fft dispatches: 16, 32, ..., 2048 and the
+ * LTE sizes 12, 24, 36, 48, 60, 72, 96, 108, 120, 144, 180, 192, 216, 240, 288, 300, 324,
+ * 360, 384, 432, 480, 540, 576, 600, 648, 720, 768, 864, 900, 960, 972, 1080, 1152, 1200.
+ * ZRX_EINVAL for any other size. */
+int zrx_fft_dev(zrx_ctx* ctx, int nfft, const struct complex16* d_in, struct complex16* d_out, int64_t count);
 
 /* d_params: 4 int32 per packet {frame_len, code_rate, soft_len, 0}; d_soft_off, d_out_off:
  * int64 byte offsets per packet; d_out_bits: int32 per packet (bits written, or -1 for a

@@ -48,10 +48,48 @@ def test_fft64_device_random_vs_oracle(engine, oracle):
 
 
 def test_fft_unsupported_size_leaves_output():
-    x = np.ones((32, 2), np.int16)
-    assert (Z.sora_fft(x) == 0).all()
+    for n in (20, 100, 4096):
+        x = np.ones((n, 2), np.int16)
+        assert (Z.sora_fft(x) == 0).all()
     assert (Z.sora_fft_dynamic(64, np.ones((64, 2), np.int16)) ==
             Z.sora_fft(np.ones((64, 2), np.int16))).all()
+
+
+def test_fft_all_sizes_kat_per_call(golden):
+    """__ext_sora_fft per call on every block of tests/libs/test_fft (all 42 sizes)."""
+    g = golden["ref_fftn"]
+    off = 0
+    for n in g["sizes"]:
+        n = int(n)
+        assert (Z.sora_fft(g["kat_in"][off:off + n]) == g["kat_out"][off:off + n]).all(), n
+        assert (Z.sora_fft_dynamic(n, g["kat_in"][off:off + n]) == g["kat_out"][off:off + n]).all(), n
+        off += n
+
+
+def test_fft_all_sizes_reference_vectors(engine, golden):
+    """zrx_fft_dev on the reference brick's outputs for random, saturating and small vectors
+    of every size (one batch per size)."""
+    g = golden["ref_fftn"]
+    o, per = g["vec_off"], int(g["vec_per"])
+    for i, n in enumerate(g["sizes"]):
+        n = int(n)
+        a, b = o[i * per], o[(i + 1) * per]
+        x = torch.from_numpy(np.ascontiguousarray(g["vec_in"][a:b].reshape(per, n, 2))).cuda()
+        assert (engine.fft(n, x).cpu().numpy().reshape(-1, 2) == g["vec_out"][a:b]).all(), n
+
+
+def test_fft_all_sizes_random_vs_oracle(engine, oracle):
+    """Batches past the kernel's grid (block-stride loop) and in-place transforms."""
+    rng = np.random.default_rng(42)
+    for n in oracle.FFT_SIZES:
+        cnt = 3000 if n <= 16 else 40
+        x = rng.integers(-32768, 32768, (cnt, n, 2)).astype(np.int16)
+        x[: cnt // 4] = rng.choice(np.array([-32768, 32767, -1, 0, 1], np.int16), (cnt // 4, n, 2))
+        exp = oracle.fft_n(n, x)
+        d = torch.from_numpy(x).cuda()
+        assert (engine.fft(n, d).cpu().numpy() == exp).all(), n
+        engine.fft(n, d, out=d)                              # aliasing in/out
+        assert (d.cpu().numpy() == exp).all(), n
 
 
 def test_v_shift_right_complex16(oracle):

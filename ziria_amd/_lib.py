@@ -40,6 +40,7 @@ SIGNATURES = [
     ("zrx_enable_timing", C.c_int, [_P, C.c_int]),
     ("zrx_get_timing", C.c_int, [_P, _P]),
     ("zrx_fft64_dev", C.c_int, [_P, _P, _P, C.c_int64]),
+    ("zrx_fft_dev", C.c_int, [_P, C.c_int, _P, _P, C.c_int64]),
     ("zrx_viterbi_dev", C.c_int, [_P, _P, _P, _P, C.c_int, _P, _P, _P]),
     ("zrx_plan_stats", C.c_int, [_P, _P]),
     ("zrx_rx_dev", C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, _P, _P]),

@@ -80,6 +80,10 @@ struct zrx_ctx {
   int32_t* fe_nsym = nullptr;
   uint32_t* fe_chan = nullptr;
   uint32_t* tx_preamble = nullptr; // 640 complex16 (TX, createPreamble.blk)
+  // FFTSafe<N> plans of every __ext_sora_fft size (zrx_fftn.hpp), built on first use
+  FftPlan* fft_plans = nullptr;
+  uint32_t* fft_tw = nullptr;
+  uint16_t* fft_pos = nullptr;
   // per-call externals
   VitStream* vstream = nullptr;
   void* small = nullptr;          // staging for single calls
@@ -360,6 +364,95 @@ static void launch_viterbi(zrx_ctx* c, const uint8_t* soft, const int64_t* soft_
         soft, soft_off, params, npkts, out, out_off, out_bits, nullptr, c->nrows, c->segs, c->dumps);
 }
 
+// ---- FFTSafe<N> plans (zrx_fftn.hpp) ------------------------------------------------
+// The sizes of __ext_sora_fft (csrc/sora_ext_lib.cpp:2672-2812), the first-stage radix of
+// each (FFTSSEEx<N> specialisations: radix 3 csrc/sora_ext_lib_fft.hpp:190-251, radix 5
+// :366-430, radix 4 otherwise, base cases 4 / 8), and the frequency index each position holds
+// after the stages (a radix-4 stage leaves residues 0, 2, 1, 3 in its quarters, radix 3 / 5
+// in order, the base cases bit-reversed) — the same recursion as oracle/ziria_oracle.c.
+static const int kFftSizeList[kFftSizes] = {16, 32, 64, 128, 256, 512, 1024, 2048, 12, 24, 36, 48, 60, 72,
+                                            96, 108, 120, 144, 180, 192, 216, 240, 288, 300, 324, 360, 384,
+                                            432, 480, 540, 576, 600, 648, 720, 768, 864, 900, 960, 972, 1080,
+                                            1152, 1200};
+static int fftn_radix(int N) {
+  switch (N) {
+    case 4: case 8: return 0;
+    case 12: case 24: case 36: case 72: case 108: case 216: case 324: case 648: case 972: return 3;
+    case 60: case 120: case 180: case 300: case 360: case 540: case 600: case 900: case 1080: return 5;
+    default: return 4;
+  }
+}
+static void fftn_freq(int N, int* idx) {
+  const int r = fftn_radix(N);
+  if (r == 0) {
+    for (int p = 0; p < N; p++) idx[p] = N == 4 ? ((p & 1) << 1 | (p >> 1)) : ((p & 1) << 2 | (p & 2) | (p >> 2));
+    return;
+  }
+  const int M = N / r;
+  std::vector<int> sub(M);
+  fftn_freq(M, sub.data());
+  static const int res4[4] = {0, 2, 1, 3};
+  for (int q = 0; q < r; q++)
+    for (int p = 0; p < M; p++) idx[q * M + p] = r * sub[p] + (r == 4 ? res4[q] : q);
+}
+// twFFTLUT{M}_{k}[n] (csrc/sora_ext_lib_fft_coeffs.hpp): round(32768 e^{-j 2 pi k n / M}),
+// each part clamped to +-32767 (the oracle's zo_twiddle, checked against the brick)
+static uint32_t fftn_twiddle(int M, int k, int n) {
+  const double ang = -2.0 * M_PI * (double)k * (double)n / (double)M;
+  double r = std::floor(32768.0 * std::cos(ang) + 0.5), i = std::floor(32768.0 * std::sin(ang) + 0.5);
+  r = std::min(32767.0, std::max(-32767.0, r));
+  i = std::min(32767.0, std::max(-32767.0, i));
+  return (uint32_t)(uint16_t)(int16_t)r | ((uint32_t)(uint16_t)(int16_t)i << 16);
+}
+static int fftn_index(int N) {
+  for (int i = 0; i < kFftSizes; i++)
+    if (kFftSizeList[i] == N) return i;
+  return -1;
+}
+static int fftn_plans(zrx_ctx* c) {
+  if (c->fft_plans) return ZRX_OK;
+  std::vector<FftPlan> plans(kFftSizes);
+  std::vector<uint32_t> tw;
+  std::vector<uint16_t> pos;
+  for (int i = 0; i < kFftSizes; i++) {
+    const int N = kFftSizeList[i];
+    FftPlan& P = plans[i];
+    P.N = N; P.nst = 0;
+    for (int M = N;;) {
+      const int r = fftn_radix(M);
+      FftStage& st = P.st[P.nst++];
+      st.radix = (uint16_t)r; st.M = (uint16_t)M; st.tw = (uint32_t)tw.size();
+      if (r == 0) break;
+      for (int k = 1; k < r; k++)
+        for (int n = 0; n < M / r; n++) tw.push_back(fftn_twiddle(M, k, n));
+      M /= r;
+    }
+    std::vector<int> idx(N);
+    fftn_freq(N, idx.data());
+    P.pos = (uint32_t)pos.size();
+    pos.resize(pos.size() + N);
+    for (int p = 0; p < N; p++) pos[P.pos + idx[p]] = (uint16_t)p;
+  }
+  ZRX_CHECK(hipSetDevice(c->device));
+  ZRX_CHECK(hipMalloc(&c->fft_plans, sizeof(FftPlan) * kFftSizes));
+  ZRX_CHECK(hipMalloc(&c->fft_tw, tw.size() * 4));
+  ZRX_CHECK(hipMalloc(&c->fft_pos, pos.size() * 2));
+  ZRX_CHECK(hipMemcpy(c->fft_plans, plans.data(), sizeof(FftPlan) * kFftSizes, hipMemcpyHostToDevice));
+  ZRX_CHECK(hipMemcpy(c->fft_tw, tw.data(), tw.size() * 4, hipMemcpyHostToDevice));
+  ZRX_CHECK(hipMemcpy(c->fft_pos, pos.data(), pos.size() * 2, hipMemcpyHostToDevice));
+  return ZRX_OK;
+}
+// count transforms of nfft points on the context's stream (nfft supported, plans built)
+static void launch_fft(zrx_ctx* c, int nfft, const void* d_in, void* d_out, int64_t count) {
+  if (nfft == 64) {
+    k_fft64<<<blocks(count, 256), 256, 0, c->stream>>>((const uint4*)d_in, (uint4*)d_out, count);
+    return;
+  }
+  const int g = (int)std::min<int64_t>(count, 8 * (int64_t)c->ncu);
+  k_fft_n<<<g, 256, 0, c->stream>>>((const uint32_t*)d_in, (uint32_t*)d_out, count, c->fft_plans + fftn_index(nfft),
+                                     c->fft_tw, c->fft_pos);
+}
+
 extern "C" {
 
 const char* zrx_version(void) { return "ziria_rx 0.1 (gfx950)"; }
@@ -407,6 +500,7 @@ int zrx_destroy(zrx_ctx* c) {
                   (void*)c->tx_preamble})
     (void)hipFree(p);
   (void)hipFree(c->vstream);
+  for (void* p : {(void*)c->fft_plans, (void*)c->fft_tw, (void*)c->fft_pos}) (void)hipFree(p);
   (void)hipFree(c->small);
   for (auto& set : c->evsets)
     for (auto& e : set) (void)hipEventDestroy(e);
@@ -494,6 +588,16 @@ int zrx_fft64_dev(zrx_ctx* c, const struct complex16* d_in, struct complex16* d_
   if (!c || nsym < 0 || (nsym > 0 && (!d_in || !d_out))) return ZRX_EINVAL;
   if (nsym == 0) return ZRX_OK;
   k_fft64<<<blocks(nsym, 256), 256, 0, c->stream>>>((const uint4*)d_in, (uint4*)d_out, nsym);
+  ZRX_CHECK(hipGetLastError());
+  return ZRX_OK;
+}
+
+int zrx_fft_dev(zrx_ctx* c, int nfft, const struct complex16* d_in, struct complex16* d_out, int64_t count) {
+  if (!c || count < 0 || fftn_index(nfft) < 0 || (count > 0 && (!d_in || !d_out))) return ZRX_EINVAL;
+  if (count == 0) return ZRX_OK;
+  const int rc = fftn_plans(c);
+  if (rc) return rc;
+  launch_fft(c, nfft, d_in, d_out, count);
   ZRX_CHECK(hipGetLastError());
   return ZRX_OK;
 }
@@ -737,20 +841,24 @@ static void* staging(zrx_ctx* c, size_t bytes) {
 
 extern "C" {
 
+// csrc/sora_ext_lib.cpp:2672-2812: every size the reference dispatches; any other prints the
+// reference's message and leaves the output untouched (:2808-2810).
 void __ext_sora_fft(struct complex16* out, int nFFTSize, struct complex16* in, int unused1) {
   (void)unused1;
-  if (nFFTSize != 64) {
-    std::printf("__ext_sora_fft error: fft size %d not supported!\n", nFFTSize);   // :2808-2810
+  if (fftn_index(nFFTSize) < 0) {
+    std::printf("__ext_sora_fft error: fft size %d not supported!\n", nFFTSize);
     return;
   }
   std::lock_guard<std::mutex> lk(g_mu);
   zrx_ctx* c = default_ctx();
-  uint8_t* d = (uint8_t*)staging(c, 512);
+  ZRX_OR_DIE(fftn_plans(c) == ZRX_OK ? hipSuccess : hipErrorUnknown);
+  const size_t bytes = (size_t)nFFTSize * 4;
+  uint8_t* d = (uint8_t*)staging(c, 2 * bytes);
   if (!d) ZRX_DIE("staging allocation failed");
-  ZRX_OR_DIE(hipMemcpyAsync(d, in, 256, hipMemcpyHostToDevice, c->stream));
-  k_fft64<<<1, 64, 0, c->stream>>>((const uint4*)d, (uint4*)(d + 256), 1);
+  ZRX_OR_DIE(hipMemcpyAsync(d, in, bytes, hipMemcpyHostToDevice, c->stream));
+  launch_fft(c, nFFTSize, d, d + bytes, 1);
   ZRX_OR_DIE(hipGetLastError());
-  ZRX_OR_DIE(hipMemcpyAsync(out, d + 256, 256, hipMemcpyDeviceToHost, c->stream));
+  ZRX_OR_DIE(hipMemcpyAsync(out, d + bytes, bytes, hipMemcpyDeviceToHost, c->stream));
   ZRX_OR_DIE(hipStreamSynchronize(c->stream));
 }
 

@@ -24,6 +24,7 @@
 #include "zrx_viterbi3.hpp"
 #include "zrx_frontend.hpp"
 #include "zrx_tx.hpp"
+#include "zrx_fftn.hpp"
 
 namespace zrx {
 

@@ -72,6 +72,15 @@ class RxEngine:
         check(lib().zrx_fft64_dev(self._h, _ptr(sym), _ptr(out), sym.numel() // 128), "zrx_fft64_dev")
         return out
 
+    def fft(self, n, x, out=None):
+        """FFTSafe<n> of every row: x int16 [..., n, 2] on the device (n any __ext_sora_fft
+        size, 12..2048)."""
+        assert x.dtype == torch.int16 and x.is_contiguous() and x.shape[-2:] == (n, 2)
+        out = torch.empty_like(x) if out is None else out
+        self._stream()
+        check(lib().zrx_fft_dev(self._h, int(n), _ptr(x), _ptr(out), x.numel() // (2 * n)), "zrx_fft_dev")
+        return out
+
     def viterbi(self, soft, soft_off, params, out, out_off, out_bits):
         """soft int8, soft_off int64 [n], params int32 [n,4] {frame_len, code_rate,
         soft_len, 0}, out uint8, out_off int64 [n], out_bits int32 [n] (all on device)."""

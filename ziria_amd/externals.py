@@ -33,9 +33,10 @@ def _c16(x, n=None):
 
 
 def sora_fft(inp):
-    """FFT of arr complex16 (re/im int16 pairs, shape [N, 2]); N = 64 on this engine.
-    For an unsupported size the reference prints an error and leaves the output
-    untouched; here the untouched output is all zeros (the Ziria caller's fresh array)."""
+    """FFT of arr complex16 (re/im int16 pairs, shape [N, 2]), N any size the reference
+    dispatches (12..2048, csrc/sora_ext_lib.cpp:2672-2812).  For another size the reference
+    prints an error and leaves the output untouched; here the untouched output is all zeros
+    (the Ziria caller's fresh array)."""
     x = _c16(inp)
     out = np.zeros_like(x)
     lib().__ext_sora_fft(_p(out), x.shape[0], _p(x), x.shape[0])
