@@ -22,8 +22,15 @@ VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9
 
 
 def short(name):
-    m = re.search(r"zrx::(?:v\d::)?(\w+)", name)
-    return m.group(1) if m else name.split("(")[0][:60]
+    """Kernel key: the function name, plus "_fix" for the seam-pass instantiation of
+    k_viterbi3 (template <0, true>), whose launches are not the decode's."""
+    m = re.search(r"zrx::(?:v\d::)?(\w+)(<[^>]*>)?", name)
+    if not m:
+        return name.split("(")[0][:60]
+    k = m.group(1)
+    if k == "k_viterbi3" and m.group(2) and "true" in m.group(2):
+        k += "_fix"
+    return k
 
 
 def read_pmc(d):

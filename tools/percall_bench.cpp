@@ -7,7 +7,7 @@
 // For each code rate: init + one decode call per data symbol's soft values (48/96/192/288
 // by modulation; here the rate's 802.11a partner modulation: 1/2 BPSK 48, 2/3 64-QAM 288,
 // 3/4 64-QAM 288), `frames` frames of frame_len bytes, random soft values.  Also
-// __ext_sora_fft(64) per call.  Prints one JSON line.
+// __ext_sora_fft per call at sizes 64, 12, 1200, 2048, 128.  Prints one JSON line.
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
@@ -51,13 +51,21 @@ int main(int argc, char** argv) {
     std::printf("%s{\"code_rate\": %d, \"soft_per_call\": %d, \"calls\": %ld, \"us_per_call\": %.2f, "
                 "\"decoded_Mbit_s\": %.3f}", cr ? ", " : "", cr, pc, calls, s / calls * 1e6, bits / s / 1e6);
   }
-  std::vector<complex16> in(64), out(64);
-  for (auto& c : in) { c.re = (int16_t)(rng() % 2001 - 1000); c.im = (int16_t)(rng() % 2001 - 1000); }
-  __ext_sora_fft(out.data(), 64, in.data(), 0);
-  const int n = 2000;
-  const auto t0 = std::chrono::steady_clock::now();
-  for (int i = 0; i < n; i++) __ext_sora_fft(out.data(), 64, in.data(), 0);
-  const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  std::printf("], \"sora_fft64\": {\"calls\": %d, \"us_per_call\": %.2f}}\n", n, s / n * 1e6);
+  // __ext_sora_fft per call at a few of its sizes (the 802.11a symbol, the smallest and
+  // largest LTE sizes, the largest power of two)
+  std::printf("], \"sora_fft\": [");
+  const int sizes[5] = {64, 12, 1200, 2048, 128};
+  for (int si = 0; si < 5; si++) {
+    const int N = sizes[si];
+    std::vector<complex16> in(N), out(N);
+    for (auto& c : in) { c.re = (int16_t)(rng() % 2001 - 1000); c.im = (int16_t)(rng() % 2001 - 1000); }
+    __ext_sora_fft(out.data(), N, in.data(), 0);
+    const int n = 1000;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < n; i++) __ext_sora_fft(out.data(), N, in.data(), 0);
+    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::printf("%s{\"size\": %d, \"calls\": %d, \"us_per_call\": %.2f}", si ? ", " : "", N, n, s / n * 1e6);
+  }
+  std::printf("]}\n");
   return 0;
 }
