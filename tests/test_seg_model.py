@@ -27,19 +27,26 @@ def test_geometry_invariants():
 
 
 def test_row_bound():
-    """sum of segments <= batch columns / L + packets for L >= columns / (64 ncu): the grid
-    of k_viterbi3's planned launch (zrx_api.hip plan_rows_max)."""
+    """sum of segments <= batch columns / L' + packets, L' = 9/8 L (uniform batch) or 11/8 L
+    (mixed, v3::kSegMixNum), L = max(1536, columns / (64 ncu)): within the grid of k_viterbi3's
+    planned launch (zrx_api.hip plan_rows_max), for mixed and uniform batches."""
     rng = np.random.default_rng(3)
-    for _ in range(200):
-        n = int(rng.integers(1, 3000))
-        fl = rng.integers(1, 4096, n)
+    ncu, mix = 256, 11
+    r = 64 * 8 * ncu // min(mix, 8)
+    for it in range(300):
+        n = int(rng.integers(1, 20000))
+        if it % 2:                                       # uniform: one frame length for all
+            fl = np.full(n, int(rng.integers(1, 4096)))
+            cols = 8 * fl + 6 + int(rng.integers(0, 300))
+        else:
+            fl = rng.integers(1, 4096, n)
+            cols = 8 * fl + 6 + rng.integers(0, 300, n)
         E = 8 * fl + 6
-        cols = E + rng.integers(0, 300, n)
-        T = int(cols.sum())
-        L = max(SM.MIN_SEG, -(-T // (64 * 256)))
-        Lb = L + L // 8
-        rows = sum(SM.seg_count(int(e), int(c), Lb) for e, c in zip(E, cols))
-        assert rows <= min(n + 64 * 256, n * SM.MAX_SEG)
+        T = int(np.sum(cols))
+        L = max(SM.MIN_SEG, -(-T // (64 * ncu)))
+        Lq = L + L // 8 if it % 2 else max(L * mix // 8, SM.MIN_SEG)
+        rows = sum(SM.seg_count(int(e), int(c), Lq) for e, c in zip(E, np.broadcast_to(cols, E.shape)))
+        assert rows <= min(n + r + r // 256 + 64, n * SM.MAX_SEG), (it, n, rows)
 
 
 CASES = [(cr, fl, noise, nseg) for cr in (0, 1, 2) for fl, noise, nseg in

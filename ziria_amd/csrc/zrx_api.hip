@@ -316,10 +316,14 @@ static int ws_release(zrx_ctx* c) {
   return ZRX_OK;
 }
 
-// Rows a plan of npkts packets can have: sum of ceil(cols / L) <= total / L + npkts with
-// total / L <= 64 ncu (k_pkt_plan), and at most kMaxSeg per packet.
+// Rows a plan of npkts packets can have: sum of ceil(cols / L') <= total / L' + npkts with
+// L' = L x kSegMixNum / 8 (mixed) or 9/8 L (uniform), total / L <= 64 ncu (k_pkt_plan), and
+// at most kMaxSeg per packet.
 static int64_t plan_rows_max(const zrx_ctx* c, int npkts) {
-  return std::min<int64_t>((int64_t)npkts + 64 * (int64_t)c->ncu, (int64_t)npkts * v3::kMaxSeg);
+  // (+ 1/256 + 64: L x kSegMixNum / 8 rounds down, which can add a few rows over the ratio)
+  // (a uniform batch is cut at 9/8 L, a mixed one at kSegMixNum / 8 L: the grid covers both)
+  const int64_t r = 64 * 8 * (int64_t)c->ncu / std::min<int64_t>(v3::kSegMixNum, 8);
+  return std::min<int64_t>((int64_t)npkts + r + r / 256 + 64, (int64_t)npkts * v3::kMaxSeg);
 }
 
 // planned: the caller already ran k_pkt_plan for this batch (rx chain)

@@ -368,7 +368,8 @@ __global__ __launch_bounds__(1024) void k_pkt_plan(const int32_t* __restrict__ v
   const uint32_t L = (uint32_t)min<uint64_t>(max<uint64_t>((tcols + rt - 1) / rt, v3::kMinSeg), 0xFFFFFFFFull);
   // (a frame is cut only when it is more than L + L / 8 long: a batch of equal frames just
   // short of four waves per SIMD stays whole)
-  const uint32_t Lb = L + L / 8u;
+  const uint32_t Lb = L + L / 8u;                       // (uniform batch)
+  const uint32_t Lm = max(L * v3::kSegMixNum / 8u, v3::kMinSeg);   // (mixed batch)
   if (uniform) {                                       // no sort: k_viterbi3 derives each row's segment
     if (t == 0) {
       const uint32_t E0 = q0.x > (1 << 21) ? 0xFFFFFFFFu : (uint32_t)q0.x * 8u + 6u;
@@ -381,12 +382,12 @@ __global__ __launch_bounds__(1024) void k_pkt_plan(const int32_t* __restrict__ v
     return;
   }
   if (ZRX_PLAN_CUT <= 2) return;
-  plan_pkts<false>(vparams, npkts, Lb, hist, order, segs, out_bits, &rtotal);
+  plan_pkts<false>(vparams, npkts, Lm, hist, order, segs, out_bits, &rtotal);
   __syncthreads();
   if (ZRX_PLAN_CUT <= 3) return;
   const uint32_t npk = order_hist_scan(hist);          // packets with rows
   __syncthreads();
-  plan_pkts<true>(vparams, npkts, Lb, hist, order, segs, out_bits, nullptr);
+  plan_pkts<true>(vparams, npkts, Lm, hist, order, segs, out_bits, nullptr);
   __syncthreads();                                     // order[] and segs[] written by the block
   if (ZRX_PLAN_CUT <= 5) return;
   // Expand: the segments of the packet at sorted position i are rows prefix(i) .. +nseg - 1

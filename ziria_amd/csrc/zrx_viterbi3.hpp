@@ -307,6 +307,15 @@ constexpr int kMaxSeg = 8;
 constexpr uint32_t kMinSeg = 1536;                     // columns per segment at least
 constexpr uint32_t kSegMaxEnd = 1u << 24;              // longer frames are not split
 constexpr uint32_t kSeamWords = 32;                    // uint2 per dump: 16 lanes x (M0, M1)
+// Segment length of a mixed batch: L x kSegMixNum / 8, L = the batch's columns / (64 rows
+// per CU); the launch grid allows 8 / kSegMixNum x 64 rows per CU + one per packet.
+// Measured on config 5 (interleaved A/B, 3 rounds): 4/8 L 0.62 ms Viterbi, 6/8 0.585, 8/8
+// 0.584, 9/8 0.578, 11/8 0.570, 14/8 0.622 — shorter segments pay more seam overlap than
+// they save in tail, longer ones leave rows above the batch's fair share.
+#ifndef ZRX_SEG_MIX_NUM
+#define ZRX_SEG_MIX_NUM 11
+#endif
+constexpr uint32_t kSegMixNum = ZRX_SEG_MIX_NUM;
 
 // floor(y / n) for n = 1..8 and y < 2^20 by a reciprocal multiply (exact there: the error
 // term y / 2^32 stays below the 1/8 gap to the next integer)
