@@ -337,7 +337,7 @@ static void launch_viterbi(zrx_ctx* c, const uint8_t* soft, const int64_t* soft_
   const bool plan = order_fits(c, npkts);
   if (plan && !planned)
     k_pkt_plan<<<1, 1024, 0, c->stream>>>(params, npkts, nullptr, nullptr, nullptr, c->rows, c->nrows, c->segs, c->order,
-                                          out_bits, c->ncu);
+                                          out_bits, c->ncu, (int)plan_rows_max(c, npkts));
   const dim3 b(256);
   const dim3 g(blocks(plan ? plan_rows_max(c, npkts) : npkts, v3::kRows));
   const int2* rows = plan ? c->rows : nullptr;
@@ -668,7 +668,7 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
   k_signal_vit<<<blocks(npkts, 4), 256, 0, s>>>(c->sig_soft, d_nsym, npkts, c->cap_nsym, c->vparams, d_info);
   const bool ordered = order_fits(c, npkts);
   k_pkt_plan<<<1, 1024, 0, s>>>(c->vparams, npkts, c->soft_off, c->dsym, c->wave_p0, ordered ? c->rows : nullptr,
-                                c->nrows, c->segs, c->order, c->dec_bits, c->ncu);
+                                c->nrows, c->segs, c->order, c->dec_bits, c->ncu, (int)plan_rows_max(c, npkts));
   if (ev) ZRX_CHECK(hipEventRecord(ev[2], s));
   // k_data_fft: waves over the batch's data symbols, at most npkts x (max_nsym - 1) of them
   const int fft_blocks = (int)std::min<int64_t>(((int64_t)npkts * (max_nsym - 1) + 255) / 256, kDataFftBlocks);

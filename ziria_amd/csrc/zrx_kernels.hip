@@ -289,7 +289,8 @@ __global__ __launch_bounds__(1024) void k_pkt_plan(const int32_t* __restrict__ v
                                                    int64_t* __restrict__ off, int32_t* __restrict__ dsym,
                                                    int32_t* __restrict__ wave_p0, int2* __restrict__ rows,
                                                    int32_t* __restrict__ nrows, uint8_t* __restrict__ segs,
-                                                   int32_t* __restrict__ order, int32_t* __restrict__ out_bits, int ncu) {
+                                                   int32_t* __restrict__ order, int32_t* __restrict__ out_bits, int ncu,
+                                                   int rows_cap) {
   __shared__ uint2 wtab[kScanPer * 16];                // (chunk i, wave w) totals, then offsets
   __shared__ uint2 round_total;
   __shared__ uint32_t hist[kOrderPerThread * 1024];
@@ -374,7 +375,7 @@ __global__ __launch_bounds__(1024) void k_pkt_plan(const int32_t* __restrict__ v
     if (t == 0) {
       const uint32_t E0 = q0.x > (1 << 21) ? 0xFFFFFFFFu : (uint32_t)q0.x * 8u + 6u;
       const uint32_t n0 = v3::seg_count(E0, cols_of(q0.y, q0.z), Lb);
-      nrows[v3::kPlanRows] = (int32_t)((uint32_t)npkts * n0);
+      nrows[v3::kPlanRows] = (int32_t)min((uint32_t)npkts * n0, (uint32_t)rows_cap);
       nrows[v3::kPlanFixes] = 0;
       nrows[v3::kPlanUniform] = (int32_t)n0;
       nrows[v3::kPlanNcu] = ncu;
@@ -414,15 +415,17 @@ __global__ __launch_bounds__(1024) void k_pkt_plan(const int32_t* __restrict__ v
     for (int w = 0; w < 16; w++) { ex += w < wv ? esum[w] : 0u; rnd += esum[w]; }
 #pragma unroll
     for (int i = 0; i < kScanPer; i++) {
-      for (uint32_t k = 0; k < ns[i]; k++)
-        rows[v3::order_place(ex + k, nfull, ncu2, ncu_rcp)] = make_int2(pk[i], (int)(k | (ns[i] << 8)));
+      for (uint32_t k = 0; k < ns[i]; k++) {
+        const uint32_t at = v3::order_place(ex + k, nfull, ncu2, ncu_rcp);
+        if (at < (uint32_t)rows_cap) rows[at] = make_int2(pk[i], (int)(k | (ns[i] << 8)));   // (always: the plan's row bound)
+      }
       ex += ns[i];
     }
     carry += rnd;
     __syncthreads();                                   // esum is rewritten by the next round
   }
   if (t == 0) {
-    nrows[v3::kPlanRows] = (int32_t)total;
+    nrows[v3::kPlanRows] = (int32_t)min(total, (uint32_t)rows_cap);
     nrows[v3::kPlanFixes] = 0;                         // counted by the seam pass
     nrows[v3::kPlanUniform] = 0;
     nrows[v3::kPlanNcu] = (int32_t)ncu2;
