@@ -276,12 +276,14 @@ def bench_mixed(args):
     expect_ok = int((m["meta"][:, 2] <= 2048).sum())
     bits = int(((inf[:, 2] - 4) * 8 * ok).sum())
     threads, host = host_cpus()
-    sample = min(256, n)
-    t0 = time.perf_counter()
+    sample = min(1024, n)
     soff, sn = m["sym_off"][:sample].cpu().numpy(), m["nsym"][:sample].cpu().numpy()
-    opay, res = O.rx_batch_time(m["sym"][:int((soff + sn).max())].cpu().numpy(), soff, sn, nthreads=threads)
+    sym_s = m["sym"][:int((soff + sn).max())].cpu().numpy()
+    opay, res = O.rx_batch_time(sym_s, soff, sn, nthreads=threads)
+    t0 = time.perf_counter()
+    _, pres = O.rx_batch_time_fast(sym_s, soff, sn, nthreads=threads)
     cpu_dt = time.perf_counter() - t0
-    cpu_bits = sum((r["len"] - 4) * 8 for r in res if r["crc_ok"])
+    cpu_bits = sum((r["len"] - 4) * 8 for r in pres if r["crc_ok"])
     oracle_match = all(int(inf[i, 4]) == r["crc_ok"] and int(inf[i, 2]) == r["len"] and
                        (not r["crc_ok"] or (pay[i, :r["len"] - 4] == opay[i, :r["len"] - 4]).all())
                        for i, r in enumerate(res))
@@ -297,7 +299,8 @@ def bench_mixed(args):
                             "oracle_sample": sample, "oracle_sample_match": bool(oracle_match)},
         "stage_ms": {k: round(v, 4) for k, v in stage.items()},
         "cpu_baseline": {"value": round(cpu_bits / cpu_dt / 1e6, 2), "unit": "Mbit/s", "cores": threads, "kind": "port",
-                         "host": host, "sample": f"first {sample} packets, {cpu_dt:.2f} s"},
+                         "host": host, "sample": f"first {sample} packets, {cpu_dt:.2f} s (CPU port: table FFT, "
+                         f"{'AVX-512' if O.rx_batch_time_fast.avx512 else 'scalar'} Viterbi, table CRC)"},
     }), flush=True)
 
 
@@ -437,9 +440,11 @@ def host_cpus():
 
 
 def cpu_baseline(b, payload_len, seconds, chan=None):
-    """The oracle (scalar C restatement, "port") on every host core this process is allowed
-    (host_cpus), packet-parallel with pthreads, over chunks of the same packets until
-    `seconds` of wall time have passed."""
+    """The chain on every host core this process is allowed (host_cpus), packet-parallel with
+    pthreads, over chunks of the same packets until `seconds` of wall time have passed: the
+    fast CPU port (oracle/cpu_port.c: table FFT, AVX-512 Viterbi, table CRC; bit-identical to
+    the oracle, tests/test_cpu_port.py) for the time-domain chain, the scalar oracle for the
+    EQ chain (the port has no channel estimator)."""
     from oracle import oracle as O
     threads, host = host_cpus()
     sym = b["sym"].cpu().numpy()
@@ -453,17 +458,20 @@ def cpu_baseline(b, payload_len, seconds, chan=None):
         lo = done % off_all.size
         hi = min(lo + chunk, off_all.size)
         if ch_all is None:
-            _, res = O.rx_batch_time(sym, off_all[lo:hi], ns_all[lo:hi], nthreads=threads)
+            _, res = O.rx_batch_time_fast(sym, off_all[lo:hi], ns_all[lo:hi], nthreads=threads)
         else:
             _, res = O.rx_batch_time_eq(sym, off_all[lo:hi], ns_all[lo:hi], ch_all[lo:hi], nthreads=threads)
         ok += sum(r["crc_ok"] for r in res)
         done += hi - lo
     dt = time.perf_counter() - t0
     bits = ok * payload_len * 8
+    what = ("scalar C oracle, EQ chain" if ch_all is not None else
+            "CPU port: table FFT, %s Viterbi, table CRC" %
+            ("AVX-512 vpermb" if getattr(O.rx_batch_time_fast, "avx512", False) else "scalar"))
     return {"value": round(bits / dt / 1e6, 2), "unit": "Mbit/s", "cores": threads, "kind": "port",
             "per_core": round(bits / dt / 1e6 / threads, 2), "host": host,
             "sample": f"{done} packets of the same batch ({ok} CRC-ok), {dt:.1f} s wall on {threads} threads "
-                      "(scalar C oracle; the reference SSE2 bricks run 41-73 Mbit/s per core, SURVEY.md §6)"}
+                      f"({what}; the reference SSE2 Viterbi brick alone runs 41-73 Mbit/s per core, SURVEY.md §6)"}
 
 
 if __name__ == "__main__":

@@ -188,6 +188,15 @@ static void batches(void) {
     CHECK(r1.crc_ok == res[p].crc_ok && memcmp(one, pay + 4096 * (size_t)p, 4096) == 0, "batch vs single %d", p);
     free(one);
   }
+  {                                                  /* the fast CPU port (bench's baseline) */
+    uint8_t* payp = calloc((size_t)N * 4096, 1);
+    zo_rx_result resp[N];
+    zp_rx_batch_time(sym, off, ns, N, payp, 4096, resp, 3);
+    for (int p = 0; p < N; p++)
+      CHECK(resp[p].crc_ok == res[p].crc_ok && resp[p].h.len == res[p].h.len &&
+            memcmp(payp + 4096 * (size_t)p, pay + 4096 * (size_t)p, 4096) == 0, "port vs oracle %d", p);
+    free(payp);
+  }
   zo_c16 chan[N * 64];
   for (int i = 0; i < N * 64; i++) { chan[i].re = 256; chan[i].im = 0; }   /* unit taps (>> 8) */
   uint8_t* pay2 = calloc((size_t)N * 4096, 1);

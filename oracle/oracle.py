@@ -262,6 +262,22 @@ def rx_batch_time(sym, sym_off, nsym, payload_stride=4096, nthreads=1):
     return pay, [_res(r) for r in res]
 
 
+def rx_batch_time_fast(sym, sym_off, nsym, payload_stride=4096, nthreads=1):
+    """rx_batch_time by the fast CPU port (oracle/cpu_port.c: table FFT, AVX-512 ACS, table
+    CRC), bit-identical to it (tests/test_cpu_port.py); bench.py's cpu_baseline leg."""
+    sym = np.ascontiguousarray(sym, np.int16)
+    sym_off = np.ascontiguousarray(sym_off, np.int64)
+    nsym = np.ascontiguousarray(nsym, np.int32)
+    n = sym_off.size
+    pay = np.zeros((n, payload_stride), np.uint8)
+    res = (RxResult * n)()
+    L = lib()
+    L.zp_rx_batch_time.restype = C.c_int
+    rx_batch_time_fast.avx512 = bool(L.zp_rx_batch_time(_p(sym), _p(sym_off), _p(nsym), n, _p(pay),
+                                                        payload_stride, res, nthreads))
+    return pay, [_res(r) for r in res]
+
+
 # ---------------------------------------------------------------- synthetic TX
 def tx_encode(bits, coding):
     bits = np.ascontiguousarray(bits, np.uint8)

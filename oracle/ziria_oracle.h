@@ -76,6 +76,10 @@ int  zo_descramble_crc(const uint8_t* decoded, int len, uint8_t* payload);
    available.  Returns 0 ok, <0 if not enough symbols.  payload must hold 4096 bytes. */
 typedef struct { zo_hdr h; int32_t crc_ok; int32_t nsym_used; int32_t viterbi_bits; } zo_rx_result;
 int zo_rx_packet_time(const zo_c16* sym, int nsym, uint8_t* payload, zo_rx_result* r);
+/* The same chain by the fast CPU port (cpu_port.c; bench.py's cpu_baseline only), identical
+   results to zo_rx_batch_time; returns 1 when its AVX-512 Viterbi ran. */
+int zp_rx_batch_time(const zo_c16* sym, const int64_t* sym_off, const int32_t* nsym, int npkts,
+                     uint8_t* payload, int payload_stride, zo_rx_result* res, int nthreads);
 /* same, fed frequency-domain data subcarriers (48 per symbol, GetData order) */
 int zo_rx_packet_freq(const zo_c16* sub48, int nsym, uint8_t* payload, zo_rx_result* r);
 

@@ -1,0 +1,36 @@
+"""The fast CPU port (oracle/cpu_port.c, bench.py's cpu_baseline leg) gives the oracle's
+results packet for packet: clean, mixed-MCS, CRC-failing, truncated and bad-header packets."""
+import numpy as np
+
+from ziria_amd import txgen
+
+
+def _same(oracle, sym, off, ns):
+    p1, r1 = oracle.rx_batch_time(sym, off, ns, nthreads=8)
+    p2, r2 = oracle.rx_batch_time_fast(sym, off, ns, nthreads=8)
+    assert r1 == r2
+    assert (p1 == p2).all()
+    return r2
+
+
+def test_port_54mbps_and_noise_edge(oracle):
+    for seed, sigma in ((3, 4.0), (9, 58.0)):
+        b = txgen.make_batch(96, seed=seed, sigma=sigma)
+        r = _same(oracle, b["sym"].numpy(), b["sym_off"].numpy(), b["nsym"].numpy())
+        assert sum(x["crc_ok"] for x in r) > 10
+
+
+def test_port_mixed_mcs(oracle):
+    m = txgen.make_mixed(128, max_len=2300, sigma=3.0, seed=21)
+    r = _same(oracle, m["sym"].numpy(), m["sym_off"].numpy(), m["nsym"].numpy())
+    assert len({(x["modulation"], x["coding"]) for x in r}) == 8
+
+
+def test_port_truncated_and_bad_header(oracle):
+    b = txgen.make_batch(8, seed=4)
+    sym = b["sym"].numpy().copy()
+    ns = b["nsym"].numpy().copy()
+    ns[1] = 10
+    S = b["max_nsym"]
+    sym[2 * S] = 0
+    _same(oracle, sym, b["sym_off"].numpy(), ns)
