@@ -136,7 +136,7 @@ def main():
     # ---------------------------------------------------------------- CPU baseline (rank 0, N=1)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(b, args.payload, args.cpu_seconds, b.get("chan"))
+        cpu = cpu_baseline(b, args.cpu_seconds, b.get("chan"))
 
     if rank == 0:
         line = {
@@ -280,10 +280,7 @@ def bench_mixed(args):
     soff, sn = m["sym_off"][:sample].cpu().numpy(), m["nsym"][:sample].cpu().numpy()
     sym_s = m["sym"][:int((soff + sn).max())].cpu().numpy()
     opay, res = O.rx_batch_time(sym_s, soff, sn, nthreads=threads)
-    t0 = time.perf_counter()
-    _, pres = O.rx_batch_time_fast(sym_s, soff, sn, nthreads=threads)
-    cpu_dt = time.perf_counter() - t0
-    cpu_bits = sum((r["len"] - 4) * 8 for r in pres if r["crc_ok"])
+    cpu = cpu_baseline(m, args.cpu_seconds)
     oracle_match = all(int(inf[i, 4]) == r["crc_ok"] and int(inf[i, 2]) == r["len"] and
                        (not r["crc_ok"] or (pay[i, :r["len"] - 4] == opay[i, :r["len"] - 4]).all())
                        for i, r in enumerate(res))
@@ -298,9 +295,7 @@ def bench_mixed(args):
         "bit_exact_check": {"crc_pass": int(ok.sum()), "expected_crc_pass": expect_ok, "payload_match": good,
                             "oracle_sample": sample, "oracle_sample_match": bool(oracle_match)},
         "stage_ms": {k: round(v, 4) for k, v in stage.items()},
-        "cpu_baseline": {"value": round(cpu_bits / cpu_dt / 1e6, 2), "unit": "Mbit/s", "cores": threads, "kind": "port",
-                         "host": host, "sample": f"first {sample} packets, {cpu_dt:.2f} s (CPU port: table FFT, "
-                         f"{'AVX-512' if O.rx_batch_time_fast.avx512 else 'scalar'} Viterbi, table CRC)"},
+        "cpu_baseline": cpu,
     }), flush=True)
 
 
@@ -439,7 +434,7 @@ def host_cpus():
                      "cpu_model": model}
 
 
-def cpu_baseline(b, payload_len, seconds, chan=None):
+def cpu_baseline(b, seconds, chan=None):
     """The chain on every host core this process is allowed (host_cpus), packet-parallel with
     pthreads, over chunks of the same packets until `seconds` of wall time have passed: the
     fast CPU port (oracle/cpu_port.c: table FFT, AVX-512 Viterbi, table CRC; bit-identical to
@@ -452,7 +447,7 @@ def cpu_baseline(b, payload_len, seconds, chan=None):
     ns_all = b["nsym"].cpu().numpy()
     ch_all = chan.cpu().numpy() if chan is not None else None
     chunk = max(1024, 64 * threads)
-    done = ok = 0
+    done = ok = bits = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         lo = done % off_all.size
@@ -462,9 +457,9 @@ def cpu_baseline(b, payload_len, seconds, chan=None):
         else:
             _, res = O.rx_batch_time_eq(sym, off_all[lo:hi], ns_all[lo:hi], ch_all[lo:hi], nthreads=threads)
         ok += sum(r["crc_ok"] for r in res)
+        bits += sum((r["len"] - 4) * 8 for r in res if r["crc_ok"])
         done += hi - lo
     dt = time.perf_counter() - t0
-    bits = ok * payload_len * 8
     what = ("scalar C oracle, EQ chain" if ch_all is not None else
             "CPU port: table FFT, %s Viterbi, table CRC" %
             ("AVX-512 vpermb" if getattr(O.rx_batch_time_fast, "avx512", False) else "scalar"))

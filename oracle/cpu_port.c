@@ -24,6 +24,9 @@
 
 /* ---------------------------------------------------------------- FFT64 with tables */
 static zo_c16 g_tw64[3][16], g_tw16[3][4];
+/* the same twiddles as madd operand pairs, 16 complex per row: [k][0] = (re, ~im) gives the
+   real part of mul_shiftx, [k][1] = (im, re) the imaginary part; stage-16 rows repeat 4x */
+static uint32_t g_w64[3][2][16] __attribute__((aligned(64))), g_w16[3][2][16] __attribute__((aligned(64)));
 static uint32_t g_crc_tab[256];
 static uint8_t g_scr_byte[128], g_scr_next[128];       /* descrambler: 8 steps from a 7-bit state */
 static uint16_t g_deint[4][288];                       /* deinterleaver source index by modulation */
@@ -33,6 +36,13 @@ static void init_tables(void) {
   for (int k = 1; k <= 3; k++) {
     for (int n = 0; n < 16; n++) zo_twiddle(64, k, n, &g_tw64[k - 1][n].re, &g_tw64[k - 1][n].im);
     for (int n = 0; n < 4; n++) zo_twiddle(16, k, n, &g_tw16[k - 1][n].re, &g_tw16[k - 1][n].im);
+    for (int n = 0; n < 16; n++) {
+      const zo_c16 a = g_tw64[k - 1][n], b = g_tw16[k - 1][n & 3];
+      g_w64[k - 1][0][n] = (uint16_t)a.re | (uint32_t)(uint16_t)~a.im << 16;
+      g_w64[k - 1][1][n] = (uint16_t)a.im | (uint32_t)(uint16_t)a.re << 16;
+      g_w16[k - 1][0][n] = (uint16_t)b.re | (uint32_t)(uint16_t)~b.im << 16;
+      g_w16[k - 1][1][n] = (uint16_t)b.im | (uint32_t)(uint16_t)b.re << 16;
+    }
   }
   for (int mod = 0; mod < 4; mod++)
     for (int k = 0; k < zo_ncbps(mod); k++) g_deint[mod][k] = (uint16_t)zo_deint_src(mod, k);
@@ -101,6 +111,59 @@ static void fft64_fast(const zo_c16* in, zo_c16* out) {
     const int b = ((i & 1) << 5) | ((i & 2) << 3) | ((i & 4) << 1) | ((i & 8) >> 1) | ((i & 16) >> 3) | ((i & 32) >> 5);
     out[i] = x[b];
   }
+}
+
+/* The same FFT64 on AVX-512, 16 complex16 values per register (the reference's FFTSSE
+   bricks hold 4 per SSE register): saturating adds, madd-wrap mul_shiftx, XOR-as-negate, so
+   the result is fft64_fast's bit for bit.  Stage 64 runs on x[0..15] .. x[48..63] as they
+   lie; a 128-bit-lane transpose puts the four 16-point sub-blocks side by side for stage 16;
+   a 32-bit transpose within lanes lines up the 4-point base cases; one permute per output
+   block undoes the bit reversal. */
+#define AVX512_FFT __attribute__((target("avx512f,avx512bw,avx512vbmi")))
+AVX512_FFT static inline __m512i v_not(__m512i x) { return _mm512_xor_si512(x, _mm512_set1_epi32(-1)); }
+AVX512_FFT static inline __m512i v_mulj(__m512i x) {      /* (re, im) -> (~im, re) */
+  return _mm512_xor_si512(_mm512_rol_epi32(x, 16), _mm512_set1_epi32(0xFFFF));
+}
+AVX512_FFT static inline __m512i v_mulw(__m512i a, const uint32_t* w) {
+  const __m512i re = _mm512_madd_epi16(a, _mm512_load_si512(w)), im = _mm512_madd_epi16(a, _mm512_load_si512(w + 16));
+  return _mm512_mask_blend_epi16(0xAAAAAAAAu, _mm512_srli_epi32(re, 15), _mm512_slli_epi32(im, 1));
+}
+AVX512_FFT static inline void v_stage(__m512i* a, __m512i* b, __m512i* c, __m512i* d, const uint32_t (*w)[2][16]) {
+  const __m512i A = _mm512_srai_epi16(*a, 2), B = _mm512_srai_epi16(*b, 2), C = _mm512_srai_epi16(*c, 2),
+                D = _mm512_srai_epi16(*d, 2);
+  const __m512i ac = _mm512_adds_epi16(A, C), bd = _mm512_adds_epi16(B, D), a_c = _mm512_subs_epi16(A, C),
+                jb = v_mulj(_mm512_subs_epi16(B, D));
+  *a = _mm512_adds_epi16(ac, bd);
+  *b = v_mulw(_mm512_subs_epi16(ac, bd), w[1][0]);
+  *c = v_mulw(_mm512_subs_epi16(a_c, jb), w[0][0]);
+  *d = v_mulw(_mm512_adds_epi16(a_c, jb), w[2][0]);
+}
+AVX512_FFT static void fft64_avx512(const zo_c16* in, zo_c16* out) {
+  __m512i y0 = _mm512_loadu_si512(in), y1 = _mm512_loadu_si512(in + 16), y2 = _mm512_loadu_si512(in + 32),
+          y3 = _mm512_loadu_si512(in + 48);
+  v_stage(&y0, &y1, &y2, &y3, g_w64);                   /* y_k = sub-block k (x[16k .. 16k+15]) */
+  const __m512i t0 = _mm512_shuffle_i64x2(y0, y1, 0x44), t1 = _mm512_shuffle_i64x2(y0, y1, 0xEE),
+                t2 = _mm512_shuffle_i64x2(y2, y3, 0x44), t3 = _mm512_shuffle_i64x2(y2, y3, 0xEE);
+  __m512i v0 = _mm512_shuffle_i64x2(t0, t2, 0x88), v1 = _mm512_shuffle_i64x2(t0, t2, 0xDD),
+          v2 = _mm512_shuffle_i64x2(t1, t3, 0x88), v3 = _mm512_shuffle_i64x2(t1, t3, 0xDD);
+  v_stage(&v0, &v1, &v2, &v3, g_w16);                   /* v_r lane k = x[16k + 4r .. 16k + 4r + 3] */
+  const __m512i u0 = _mm512_unpacklo_epi32(v0, v1), u1 = _mm512_unpackhi_epi32(v0, v1),
+                u2 = _mm512_unpacklo_epi32(v2, v3), u3 = _mm512_unpackhi_epi32(v2, v3);
+  const __m512i e0 = _mm512_srai_epi16(_mm512_unpacklo_epi64(u0, u2), 2),
+                e1 = _mm512_srai_epi16(_mm512_unpackhi_epi64(u0, u2), 2),
+                e2 = _mm512_srai_epi16(_mm512_unpacklo_epi64(u1, u3), 2),
+                e3 = _mm512_srai_epi16(_mm512_unpackhi_epi64(u1, u3), 2);   /* e_i[4k + r] = x[16k + 4r + i] */
+  const __m512i A = _mm512_adds_epi16(e0, e2), B = _mm512_adds_epi16(e1, e3);  /* FFTSSEEx<4>, as fft4 */
+  const __m512i L = _mm512_adds_epi16(e0, v_not(e2)), T = _mm512_adds_epi16(e1, v_not(e3));
+  const __m512i jT = v_mulj(T);
+  const __m512i f[4] = {_mm512_adds_epi16(A, B), _mm512_adds_epi16(v_not(B), A), _mm512_adds_epi16(L, v_not(jT)),
+                        _mm512_adds_epi16(L, jT)};
+  /* out[k] = x[bitrev6(k)]: block k >> 4 = 2 k5 + k4 comes from f[2 k4 + k5], element bitrev4(k & 15) */
+  const __m512i rev4 = _mm512_setr_epi32(0, 8, 4, 12, 2, 10, 6, 14, 1, 9, 5, 13, 3, 11, 7, 15);
+  _mm512_storeu_si512(out, _mm512_permutexvar_epi32(rev4, f[0]));
+  _mm512_storeu_si512(out + 16, _mm512_permutexvar_epi32(rev4, f[2]));
+  _mm512_storeu_si512(out + 32, _mm512_permutexvar_epi32(rev4, f[1]));
+  _mm512_storeu_si512(out + 48, _mm512_permutexvar_epi32(rev4, f[3]));
 }
 
 /* GetData (GetData.blk:24-35) >>> DemapLimit >>> Demap >>> Deinterleave of one FFT output,
@@ -264,7 +327,7 @@ static void rx_packet(const zo_c16* sym, int nsym, uint8_t* payload, zo_rx_resul
   if (nsym < 1) return;
   zo_c16 f[64], sub[48], lim[48];
   int8_t soft[288], di[288];
-  fft64_fast(sym, f);                                  /* SIGNAL: DecodePLCP.blk:30-37 */
+  if (g_avx) fft64_avx512(sym, f); else fft64_fast(sym, f);   /* SIGNAL: DecodePLCP.blk:30-37 */
   zo_get_data(f, sub);
   zo_demap_limit(sub, 48, lim);
   zo_demap(0, lim, soft);
@@ -285,7 +348,7 @@ static void rx_packet(const zo_c16* sym, int nsym, uint8_t* payload, zo_rx_resul
     zo_vit_init(zv, len + 2, cod, 256);
   }
   for (int k = 0; k < nsym - 1 && bits < (len + 2) * 8; k++) {
-    fft64_fast(sym + 64 * (1 + k), f);
+    if (g_avx) fft64_avx512(sym + 64 * (1 + k), f); else fft64_fast(sym + 64 * (1 + k), f);
     symbol_soft(f, mod, di);
     for (int c = 0; c < nc; c += 48)
       bits += g_avx ? pv_decode_avx512(v, di + c, 48, dec + bits / 8) : zo_vit_decode(zv, di + c, 48, dec + bits / 8);
@@ -299,7 +362,8 @@ static void rx_packet(const zo_c16* sym, int nsym, uint8_t* payload, zo_rx_resul
 
 typedef struct {
   const zo_c16* sym; const int64_t* off; const int32_t* n;
-  uint8_t* out; int stride; zo_rx_result* res; int npkts, t, nt;
+  uint8_t* out; int stride; zo_rx_result* res; int npkts;
+  int* next;                                           /* shared packet counter (dynamic claim) */
 } pjob_t;
 static void* pworker(void* p) {
   pjob_t* j = (pjob_t*)p;
@@ -307,13 +371,22 @@ static void* pworker(void* p) {
   v.cap = 40000 + 8;
   v.surv = (uint64_t*)calloc(v.cap, sizeof(uint64_t));
   zo_vit zv; memset(&zv, 0, sizeof(zv));
-  for (int i = j->t; i < j->npkts; i += j->nt)
+  for (int i; (i = __atomic_fetch_add(j->next, 1, __ATOMIC_RELAXED)) < j->npkts;)
     rx_packet(j->sym + 64 * j->off[i], j->n[i], j->out + (size_t)i * j->stride, &j->res[i], &v, &zv);
   free(v.surv);
   zo_vit_free(&zv);
   return 0;
 }
 static void init_all(void) { init_tables(); init_vit_tables(); g_avx = have_avx512(); }
+
+/* n FFT64s by the port's own FFT (tests/test_cpu_port.py compares them with the oracle's) */
+int zp_fft64(const zo_c16* in, zo_c16* out, int n) {
+  pthread_once(&g_once, init_all);
+  for (int i = 0; i < n; i++) {
+    if (g_avx) fft64_avx512(in + 64 * i, out + 64 * i); else fft64_fast(in + 64 * i, out + 64 * i);
+  }
+  return g_avx;
+}
 
 /* Same contract as zo_rx_batch_time.  Returns 1 when the AVX-512 ACS ran, 0 otherwise. */
 int zp_rx_batch_time(const zo_c16* sym, const int64_t* sym_off, const int32_t* nsym, int npkts,
@@ -323,8 +396,9 @@ int zp_rx_batch_time(const zo_c16* sym, const int64_t* sym_off, const int32_t* n
   if (nthreads > 256) nthreads = 256;
   pthread_t th[256];
   pjob_t jobs[256];
+  int next = 0;
   for (int t = 0; t < nthreads; t++) {
-    pjob_t j = {sym, sym_off, nsym, payload, payload_stride, res, npkts, t, nthreads};
+    pjob_t j = {sym, sym_off, nsym, payload, payload_stride, res, npkts, &next};
     jobs[t] = j;
   }
   for (int t = 1; t < nthreads; t++) pthread_create(&th[t], 0, pworker, &jobs[t]);

@@ -1,5 +1,7 @@
 """The fast CPU port (oracle/cpu_port.c, bench.py's cpu_baseline leg) gives the oracle's
 results packet for packet: clean, mixed-MCS, CRC-failing, truncated and bad-header packets."""
+import ctypes
+
 import numpy as np
 
 from ziria_amd import txgen
@@ -34,3 +36,16 @@ def test_port_truncated_and_bad_header(oracle):
     S = b["max_nsym"]
     sym[2 * S] = 0
     _same(oracle, sym, b["sym_off"].numpy(), ns)
+
+
+def test_port_fft64_vs_oracle(oracle):
+    rng = np.random.default_rng(5)
+    x = rng.integers(-32768, 32768, size=(3000, 64, 2), dtype=np.int16)
+    x[:500] = rng.choice(np.array([-32768, 32767, -1, 0], np.int16), size=(500, 64, 2))
+    x[500:1000] >>= 6
+    got = np.zeros_like(x)
+    L = oracle.lib()
+    L.zp_fft64.restype = ctypes.c_int
+    L.zp_fft64(oracle._p(x), oracle._p(got), x.shape[0])
+    want = oracle.fft64(x.reshape(-1, 64, 2))
+    assert (got == want.reshape(got.shape)).all()
