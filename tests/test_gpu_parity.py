@@ -175,6 +175,25 @@ def test_viterbi_per_call_depths_vs_oracle(oracle):
             assert nb == 8 * exp.size and (got == exp).all(), (cr, fl, depth, call, k)
 
 
+def test_viterbi_per_call_deep_windows_vs_oracle(oracle):
+    """Depths whose traceback window (depth + 24..31 lookahead columns) fits the per-call
+    kernel's 4096-column LDS window, straddles it, and exceeds it (walked in device memory)."""
+    from tests.golden import synth
+    for cr, depth, call in ((0, 4060, 480), (2, 4070, 96), (0, 5000, 480), (1, 8000, 4800)):
+        s = synth.viterbi_soft(cr, 2000, 3, seed=depth)
+        Z.viterbi_brick_init_fast(2000, cr, depth)
+        d = oracle.Viterbi()
+        d.init(2000, cr, depth)
+        total = 0
+        for k in range(0, s.size - call + 1, call):
+            c = np.ascontiguousarray(s[k:k + call])
+            nb, got = Z.viterbi_brick_decode_fast(c)
+            exp = d.decode(c)
+            assert nb == 8 * exp.size and (got == exp).all(), (cr, depth, call, k)
+            total += exp.size
+        assert total >= depth // 8, (cr, depth, total)
+
+
 def test_viterbi_batch_random_vs_oracle(oracle):
     rng = np.random.default_rng(77)
     softs, offs, fls, crs = [], [0], [], []

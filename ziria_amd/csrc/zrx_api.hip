@@ -88,6 +88,9 @@ struct zrx_ctx {
   VitStream* vstream = nullptr;
   void* small = nullptr;          // staging for single calls
   size_t small_cap = 0;
+  uint8_t* hsmall = nullptr;      // pinned, device-mapped staging the per-call kernels read and write in place
+  uint8_t* hsmall_dev = nullptr;
+  size_t hsmall_cap = 0;
 };
 
 static int check_device(int device) {
@@ -506,6 +509,7 @@ int zrx_destroy(zrx_ctx* c) {
   (void)hipFree(c->vstream);
   for (void* p : {(void*)c->fft_plans, (void*)c->fft_tw, (void*)c->fft_pos}) (void)hipFree(p);
   (void)hipFree(c->small);
+  if (c->hsmall) (void)hipHostFree(c->hsmall);
   for (auto& set : c->evsets)
     for (auto& e : set) (void)hipEventDestroy(e);
   if (c->ws_free) (void)hipEventDestroy(c->ws_free);
@@ -835,6 +839,31 @@ static void* staging(zrx_ctx* c, size_t bytes) {
   return c->small;
 }
 
+// Pinned host memory mapped into the device's address space (coherent: the GPU does not
+// cache it), so a per-call external's kernel reads its input and writes its output in place:
+// one launch and one stream sync per call, no DMA copies (each costs ~10 us at this size).
+static void* pinned_mapped(size_t bytes, void** dev) {
+  void* h = nullptr;
+  if (hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
+  if (hipHostGetDevicePointer(dev, h, 0) != hipSuccess) { (void)hipHostFree(h); return nullptr; }
+  return h;
+}
+static uint8_t* hstaging(zrx_ctx* c, size_t bytes, uint8_t** dev) {
+  if (bytes > c->hsmall_cap) {
+    if (c->hsmall) (void)hipHostFree(c->hsmall);
+    c->hsmall = nullptr;
+    c->hsmall_cap = 0;
+    const size_t cap = std::max<size_t>(bytes, 1 << 16);
+    void* dp = nullptr;
+    c->hsmall = (uint8_t*)pinned_mapped(cap, &dp);
+    if (!c->hsmall) return nullptr;
+    c->hsmall_dev = (uint8_t*)dp;
+    c->hsmall_cap = cap;
+  }
+  *dev = c->hsmall_dev;
+  return c->hsmall;
+}
+
 #define ZRX_DIE(msg)                                                     \
   do {                                                                   \
     std::fprintf(stderr, "ziria_rx: %s (%s:%d)\n", msg, __FILE__, __LINE__); \
@@ -857,13 +886,14 @@ void __ext_sora_fft(struct complex16* out, int nFFTSize, struct complex16* in, i
   zrx_ctx* c = default_ctx();
   ZRX_OR_DIE(fftn_plans(c) == ZRX_OK ? hipSuccess : hipErrorUnknown);
   const size_t bytes = (size_t)nFFTSize * 4;
-  uint8_t* d = (uint8_t*)staging(c, 2 * bytes);
-  if (!d) ZRX_DIE("staging allocation failed");
-  ZRX_OR_DIE(hipMemcpyAsync(d, in, bytes, hipMemcpyHostToDevice, c->stream));
+  uint8_t* d = nullptr;
+  uint8_t* h = hstaging(c, 2 * bytes, &d);
+  if (!h) ZRX_DIE("pinned staging allocation failed");
+  std::memcpy(h, in, bytes);
   launch_fft(c, nFFTSize, d, d + bytes, 1);
   ZRX_OR_DIE(hipGetLastError());
-  ZRX_OR_DIE(hipMemcpyAsync(out, d + bytes, bytes, hipMemcpyDeviceToHost, c->stream));
   ZRX_OR_DIE(hipStreamSynchronize(c->stream));
+  std::memcpy(out, h + bytes, bytes);
 }
 
 void __ext_sora_fft_dynamic(struct complex16* out, int unused2, int16_t nFFTSize, struct complex16* in, int unused1) {
@@ -881,9 +911,11 @@ struct VitHost {
   bool ready = false;
   uint32_t tr = 0, ob = 0, tr_end = 0, depth = 256;
   int cr = 0;
-  uint8_t* pend = nullptr;         // queued soft values (pinned)
+  uint8_t* pend = nullptr;         // queued soft values (pinned, mapped: the kernel reads them in place)
+  uint8_t* pend_dev = nullptr;
   size_t npend = 0, cap = 0;
-  uint8_t* out = nullptr;          // pinned copy-back buffer
+  uint8_t* out = nullptr;          // pinned, mapped: the kernel writes the call's bytes here, bit count at the end
+  uint8_t* out_dev = nullptr;
   size_t out_cap = 0;
 };
 static VitHost g_vh;
@@ -929,31 +961,29 @@ int16_t __ext_viterbi_brick_decode_fast(int8_t* intInput, int len1, unsigned cha
     else if (h.tr >= h.ob + h.depth + 30u) cnt = h.depth;
     if (cnt) { bytes += cnt >> 3; h.ob += cnt; }
   }
-  if (h.npend + n > h.cap) {
-    const size_t cap = std::max<size_t>(h.npend + n, std::max<size_t>(2 * h.cap, 1 << 16));
-    uint8_t* np = nullptr;
-    ZRX_OR_DIE(hipHostMalloc((void**)&np, cap, hipHostMallocDefault));
+  if (h.npend + n + 64 > h.cap) {                    // +64: the kernel reads whole dwords past the end
+    const size_t cap = std::max<size_t>(h.npend + n + 64, std::max<size_t>(2 * h.cap, 1 << 16));
+    void* dp = nullptr;
+    uint8_t* np = (uint8_t*)pinned_mapped(cap, &dp);
+    if (!np) ZRX_DIE("pinned allocation failed");
     if (h.npend) std::memcpy(np, h.pend, h.npend);
     if (h.pend) (void)hipHostFree(h.pend);
-    h.pend = np; h.cap = cap;
+    h.pend = np; h.pend_dev = (uint8_t*)dp; h.cap = cap;
   }
   std::memcpy(h.pend + h.npend, intInput, n);
   h.npend += n;
   if (bytes == 0) return 0;                          // no traceback in this call: stays queued
-  const size_t out_cap = (size_t)h.npend + 512;      // bytes the queued groups can emit at most
-  uint8_t* d = (uint8_t*)staging(c, h.npend + out_cap + 64);
-  if (!d) ZRX_DIE("staging allocation failed");
-  uint8_t* d_out = d + ((h.npend + 15) / 16) * 16;
-  int32_t* d_bits = (int32_t*)(d_out + out_cap);
-  if (bytes > h.out_cap) {
+  if (bytes + 16 > h.out_cap) {
     if (h.out) (void)hipHostFree(h.out);
-    h.out_cap = std::max<size_t>(bytes, 4096);
-    ZRX_OR_DIE(hipHostMalloc((void**)&h.out, h.out_cap, hipHostMallocDefault));
+    h.out_cap = std::max<size_t>(((bytes + 15) / 16) * 16 + 16, 4096);
+    void* dp = nullptr;
+    h.out = (uint8_t*)pinned_mapped(h.out_cap, &dp);
+    if (!h.out) ZRX_DIE("pinned allocation failed");
+    h.out_dev = (uint8_t*)dp;
   }
-  ZRX_OR_DIE(hipMemcpyAsync(d, h.pend, h.npend, hipMemcpyHostToDevice, c->stream));
-  k_viterbi_stream<<<1, 64, 0, c->stream>>>(c->vstream, d, (int)h.npend, d_out, d_bits);
+  k_viterbi_stream<<<1, 64, 0, c->stream>>>(c->vstream, h.pend_dev, (int)h.npend, h.out_dev,
+                                            (int32_t*)(h.out_dev + h.out_cap - 16));
   ZRX_OR_DIE(hipGetLastError());
-  ZRX_OR_DIE(hipMemcpyAsync(h.out, d_out, bytes, hipMemcpyDeviceToHost, c->stream));
   ZRX_OR_DIE(hipStreamSynchronize(c->stream));
   std::memcpy(bit, h.out, bytes);
   h.npend = 0;
@@ -964,13 +994,14 @@ int16_t __ext_viterbiSig11a_brick_decode_fast(int8_t* intInput, int len1, unsign
   (void)len1; (void)len2;
   std::lock_guard<std::mutex> lk(g_mu);
   zrx_ctx* c = default_ctx();
-  uint8_t* d = (uint8_t*)staging(c, 128);
-  if (!d) ZRX_DIE("staging allocation failed");
-  ZRX_OR_DIE(hipMemcpyAsync(d, intInput, 48, hipMemcpyHostToDevice, c->stream));
+  uint8_t* d = nullptr;
+  uint8_t* h = hstaging(c, 128, &d);
+  if (!h) ZRX_DIE("pinned staging allocation failed");
+  std::memcpy(h, intInput, 48);
   k_sig_bytes<<<1, 64, 0, c->stream>>>((const uint32_t*)d, 1, d + 64);
   ZRX_OR_DIE(hipGetLastError());
-  ZRX_OR_DIE(hipMemcpyAsync(bit, d + 64, 3, hipMemcpyDeviceToHost, c->stream));
   ZRX_OR_DIE(hipStreamSynchronize(c->stream));
+  std::memcpy(bit, h + 64, 3);
   uint32_t w;
   std::memcpy(&w, bit, 4);
   w >>= 6;                                            // *((unum32 *)bit) >>= 6  (:191)

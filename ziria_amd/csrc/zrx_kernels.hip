@@ -769,9 +769,52 @@ __device__ __forceinline__ void stream_step(VitRun& v, int a, int b, const VitLa
   if (lane == 0 && v.tr < (uint32_t)(kTrellisMax + 16))
     __hip_atomic_store(st->surv + v.tr, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Survivor words of columns lo .. lo + n - 1 staged in LDS for one traceback.
+struct SurvWin {
+  const uint64_t* w;
+  uint32_t lo;
+  __device__ __forceinline__ uint64_t operator()(uint32_t t) const { return w[t - lo]; }
+};
+constexpr uint32_t kStreamWin = 4096;   // LDS window (32 KB): depth + lookahead up to 4096 columns
+
+// Normalize and traceback schedule as vit_after_group; the traceback window (its cnt + look
+// columns, written to device memory by lane 0 in this or an earlier call) is first copied
+// into LDS by the whole wave, so the walk's dependent reads are LDS reads, not L2 round trips.
+// A window beyond kStreamWin (depth > ~4060) walks device memory.
+__device__ __forceinline__ void stream_after_group(VitRun& v, int lane, const VitStream* st, uint64_t* win,
+                                                   uint8_t* __restrict__ out) {
+  if ((v.tr & 7u) == 0) v.m = vit_normalize(v.m);
+  uint32_t cnt = 0, look = 0;
+  if (v.tr >= v.tr_end) {
+    cnt = v.tr_end - v.ob - 6u;
+    look = v.tr - v.tr_end;
+  } else if (v.tr >= v.ob + v.depth + 30u) {
+    cnt = v.depth;
+    look = 24u + (v.tr - (v.ob + v.depth + 30u)) % 8u;
+  }
+  if (!cnt) return;
+  const uint32_t n = cnt + look, lo = v.tr - n;      // columns the walk reads: lo .. tr - 1
+  __builtin_amdgcn_s_waitcnt(0);                     // this wave's survivor stores have completed
+  if (n <= kStreamWin) {
+    for (uint32_t j = (uint32_t)lane; j < n; j += 64)
+      win[j] = __hip_atomic_load(st->surv + lo + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    vit_traceback(v.m, v.tr, cnt, look, lane, SurvWin{win, lo}, out + v.total_bytes);
+    __syncthreads();                                   // the window is rewritten by the next traceback
+  } else {
+    vit_traceback(v.m, v.tr, cnt, look, lane, SurvGlobal{st->surv}, out + v.total_bytes);
+  }
+  v.ob += cnt;
+  v.total_bytes += cnt >> 3;
+}
+
 // One decode call on n soft values (one wave).  out gets this call's bytes; *out_bits its bits.
-__global__ void k_viterbi_stream(VitStream* st, const uint8_t* __restrict__ sp, int n, uint8_t* __restrict__ out,
-                                 int32_t* __restrict__ out_bits) {
+// Soft values are read 192 at a time (48 dwords, one per lane; 192 is a multiple of every
+// group size) and taken out with readlane, so no group waits on a memory load; the bytes and
+// the bit count go straight to the caller's pinned buffer.
+__global__ __launch_bounds__(64) void k_viterbi_stream(VitStream* st, const uint8_t* __restrict__ sp, int n,
+                                                       uint8_t* __restrict__ out, int32_t* __restrict__ out_bits) {
+  __shared__ uint64_t win[kStreamWin];
   const int lane = threadIdx.x;
   const VitLane L = vit_lane(lane);
   VitRun v;
@@ -780,16 +823,24 @@ __global__ void k_viterbi_stream(VitStream* st, const uint8_t* __restrict__ sp, 
   v.tr_end = st->frame_len * 8u + 6u; v.depth = st->depth; v.done = false;
   const int cr = (int)st->code_rate;
   const int G = cr == 0 ? 2 : (cr == 1 ? 3 : (cr == 2 ? 4 : 0));
+  // sp is pinned host memory (the host keeps it 16-B aligned with 64 B of slack): the next
+  // chunk's load is issued before this chunk's groups, so its latency hides behind them.
+  auto load = [sp, n, lane](int base) {
+    return (lane < 48 && base + 4 * lane < n) ? (int)((const uint32_t*)(sp + base))[lane] : 0;
+  };
   if (G) {
-    for (int k = 0; k + G <= n; k += G) {
-      const int a = sp[k], b = sp[k + 1];
-      stream_step<3>(v, a, b, L, lane, st);
-      if (cr == 2) { stream_step<1>(v, sp[k + 2], 0, L, lane, st); stream_step<2>(v, sp[k + 3], 0, L, lane, st); }
-      if (cr == 1) { stream_step<1>(v, sp[k + 2], 0, L, lane, st); }
-      __builtin_amdgcn_s_waitcnt(0);
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-      v.done = false;   // the brick keeps running after the final traceback (output 0 bits)
-      vit_after_group(v, lane, SurvGlobal{st->surv}, out);
+    int next = load(0);
+    for (int base = 0; base + G <= n; base += 192) {
+      const int chunk = next;
+      next = load(base + 192);
+      const int cn = min(192, n - base);
+      auto soft = [chunk](int q) { return (int)(((uint32_t)__builtin_amdgcn_readlane(chunk, q >> 2) >> (8 * (q & 3))) & 0xFFu); };
+      for (int k = 0; k + G <= cn; k += G) {
+        stream_step<3>(v, soft(k), soft(k + 1), L, lane, st);
+        if (cr == 2) { stream_step<1>(v, soft(k + 2), 0, L, lane, st); stream_step<2>(v, soft(k + 3), 0, L, lane, st); }
+        if (cr == 1) { stream_step<1>(v, soft(k + 2), 0, L, lane, st); }
+        stream_after_group(v, lane, st, win, out);   // the brick keeps running after the final traceback (0 bits)
+      }
     }
   }
   st->m[lane] = v.m;
