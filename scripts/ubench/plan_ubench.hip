@@ -21,7 +21,7 @@ static void run(const char* name, const std::vector<int32_t>& vp, int npkts, boo
   hipEvent_t a, b;
   hipEventCreate(&a); hipEventCreate(&b);
   auto launch = [&]() {
-    k_pkt_plan<<<1, 1024>>>(d_vp, npkts, chain ? d_off : nullptr, d_dsym, d_w, d_rows, d_nrows, d_segs, d_order, d_bits, 256, npkts + 16384);
+    k_pkt_plan<<<1, 1024>>>(d_vp, npkts, chain ? d_off : nullptr, d_dsym, d_w, d_rows, d_nrows, d_segs, d_order, d_bits, 256, npkts + 16384, 0, nullptr);
   };
   for (int i = 0; i < 5; i++) launch();
   hipEventRecord(a);

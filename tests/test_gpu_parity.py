@@ -464,3 +464,27 @@ def test_chain_large_batch_properties(engine):
     info = info.cpu().numpy()
     assert (info[:, 4] == 1).all()
     assert (pay[:, :1500].cpu().numpy() == b["payload"]).all()
+
+
+def test_chain_split_plan_alternating_batches(engine):
+    """The rx chain sorts a mixed batch's rows beside k_data_fft only when the previous batch
+    was mixed (k_pkt_plan's host-mapped hint), otherwise inline: mixed and uniform batches in
+    turn on one engine take both paths, from fresh and stale hints, with identical results."""
+    m = txgen.make_mixed_fast(2048, min_len=64, max_len=2300, sigma=3.0, seed=77, device="cuda")
+    u = txgen.make_batch(1024, seed=78, sigma=4.0, device="cuda")
+    engine.reserve(2048, max(m["max_nsym"], u["max_nsym"]))
+    runs = {"m": [], "u": []}
+    for k in "mmumuum":
+        b = m if k == "m" else u
+        pay, info = engine.rx(b["sym"], b["sym_off"], b["nsym"], b["max_nsym"])
+        torch.cuda.synchronize()
+        runs[k].append((pay.cpu().numpy().copy(), info.cpu().numpy().copy()))
+    for k, rs in runs.items():
+        for pay, info in rs[1:]:
+            assert (pay == rs[0][0]).all() and (info == rs[0][1]).all(), k
+    pay, info = runs["m"][0]
+    valid = m["meta"][:, 2] <= 2048
+    assert (info[valid, 4] == 1).all()
+    for i in np.nonzero(valid)[0][:512]:
+        assert (pay[i, :m["meta"][i, 2] - 4] == m["payload"][i]).all(), i
+    assert (runs["u"][0][1][:, 4] == 1).all()

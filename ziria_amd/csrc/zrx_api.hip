@@ -88,6 +88,10 @@ struct zrx_ctx {
   VitStream* vstream = nullptr;
   void* small = nullptr;          // staging for single calls
   size_t small_cap = 0;
+  hipStream_t side = nullptr;     // k_pkt_rows beside k_data_fft (rx chain, mixed batches)
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  int32_t* mixed_hint = nullptr;  // pinned, mapped: 1 when the last planned batch was mixed
+  int32_t* mixed_hint_dev = nullptr;
   uint8_t* hsmall = nullptr;      // pinned, device-mapped staging the per-call kernels read and write in place
   uint8_t* hsmall_dev = nullptr;
   size_t hsmall_cap = 0;
@@ -340,7 +344,7 @@ static void launch_viterbi(zrx_ctx* c, const uint8_t* soft, const int64_t* soft_
   const bool plan = order_fits(c, npkts);
   if (plan && !planned)
     k_pkt_plan<<<1, 1024, 0, c->stream>>>(params, npkts, nullptr, nullptr, nullptr, c->rows, c->nrows, c->segs, c->order,
-                                          out_bits, c->ncu, (int)plan_rows_max(c, npkts));
+                                          out_bits, c->ncu, (int)plan_rows_max(c, npkts), 0, nullptr);
   const dim3 b(256);
   const dim3 g(blocks(plan ? plan_rows_max(c, npkts) : npkts, v3::kRows));
   const int2* rows = plan ? c->rows : nullptr;
@@ -510,9 +514,15 @@ int zrx_destroy(zrx_ctx* c) {
   for (void* p : {(void*)c->fft_plans, (void*)c->fft_tw, (void*)c->fft_pos}) (void)hipFree(p);
   (void)hipFree(c->small);
   if (c->hsmall) (void)hipHostFree(c->hsmall);
+  if (c->mixed_hint) (void)hipHostFree(c->mixed_hint);
   for (auto& set : c->evsets)
     for (auto& e : set) (void)hipEventDestroy(e);
   if (c->ws_free) (void)hipEventDestroy(c->ws_free);
+  if (c->side) {
+    (void)hipStreamDestroy(c->side);
+    (void)hipEventDestroy(c->ev_fork);
+    (void)hipEventDestroy(c->ev_join);
+  }
   delete c;
   return ZRX_OK;
 }
@@ -569,7 +579,7 @@ int zrx_reserve(zrx_ctx* c, int npkts, int max_nsym) {
   ZRX_CHECK(hipMalloc(&c->dec_bits, (size_t)np * 4 + 4));
   c->rows_cap = plan_rows_max(c, np);
   ZRX_CHECK(hipMalloc(&c->rows, (size_t)c->rows_cap * 8 + 8));
-  ZRX_CHECK(hipMalloc(&c->nrows, 16));
+  ZRX_CHECK(hipMalloc(&c->nrows, 32));
   ZRX_CHECK(hipMalloc(&c->segs, (size_t)np + 16));
   ZRX_CHECK(hipMalloc(&c->order, (size_t)np * 4 + 16));
   ZRX_CHECK(hipMalloc(&c->dumps, (size_t)np * (v3::kMaxSeg - 1) * 2 * v3::kSeamWords * 8 + 256));
@@ -631,6 +641,7 @@ int zrx_viterbi_dev(zrx_ctx* c, const int8_t* d_soft, const int64_t* d_soft_off,
   return ws_release(c);
 }
 
+static void* pinned_mapped(size_t bytes, void** dev);
 static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_sym_off, const int32_t* d_nsym,
                     int npkts, int max_nsym, const struct complex16* d_chan, uint8_t* d_payload, int32_t* d_info) {
   if (!c || npkts < 0 || max_nsym < 1) return ZRX_EINVAL;
@@ -671,8 +682,35 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
   if (ev) ZRX_CHECK(hipEventRecord(ev[1], s));
   k_signal_vit<<<blocks(npkts, 4), 256, 0, s>>>(c->sig_soft, d_nsym, npkts, c->cap_nsym, c->vparams, d_info);
   const bool ordered = order_fits(c, npkts);
+  // A mixed batch's sort and row expansion (k_pkt_rows) only feed the Viterbi, so they can run
+  // on a side stream while k_data_fft runs (config 5: -27 us a batch).  The fork and join cost
+  // ~19 us of queue latency (config 3: +19 us) and a uniform batch has nothing to sort, so the
+  // plan is split only when the previous batch was mixed (k_pkt_plan writes that to a mapped
+  // host word; a stale read only picks the slower path: either way the rows are exact).
+  if (!c->mixed_hint) {
+    void* dp = nullptr;
+    c->mixed_hint = (int32_t*)pinned_mapped(64, &dp);
+    if (!c->mixed_hint) return ZRX_ENOMEM;
+    c->mixed_hint_dev = (int32_t*)dp;
+    *(volatile int32_t*)c->mixed_hint = 0;
+  }
+  const bool split = ordered && *(volatile int32_t*)c->mixed_hint != 0;
   k_pkt_plan<<<1, 1024, 0, s>>>(c->vparams, npkts, c->soft_off, c->dsym, c->wave_p0, ordered ? c->rows : nullptr,
-                                c->nrows, c->segs, c->order, c->dec_bits, c->ncu, (int)plan_rows_max(c, npkts));
+                                c->nrows, c->segs, c->order, c->dec_bits, c->ncu, (int)plan_rows_max(c, npkts),
+                                split ? 1 : 0, ordered ? c->mixed_hint_dev : nullptr);
+  if (split) {
+    if (!c->side) {
+      ZRX_CHECK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+      // (stream-to-stream on one device: no system-scope fence, which writes back the L2s)
+      ZRX_CHECK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming | hipEventDisableSystemFence));
+      ZRX_CHECK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming | hipEventDisableSystemFence));
+    }
+    ZRX_CHECK(hipEventRecord(c->ev_fork, s));
+    ZRX_CHECK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+    k_pkt_rows<<<1, 1024, 0, c->side>>>(c->vparams, npkts, c->rows, c->nrows, c->segs, c->order, c->dec_bits, c->ncu,
+                                        (int)plan_rows_max(c, npkts));
+    ZRX_CHECK(hipEventRecord(c->ev_join, c->side));
+  }
   if (ev) ZRX_CHECK(hipEventRecord(ev[2], s));
   // k_data_fft: waves over the batch's data symbols, at most npkts x (max_nsym - 1) of them
   const int fft_blocks = (int)std::min<int64_t>(((int64_t)npkts * (max_nsym - 1) + 255) / 256, kDataFftBlocks);
@@ -685,6 +723,7 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
                                                     c->soft_off, c->dsym, c->wave_p0, chan, T);
   }
   if (ev) ZRX_CHECK(hipEventRecord(ev[3], s));
+  if (split) ZRX_CHECK(hipStreamWaitEvent(s, c->ev_join, 0));
   launch_viterbi(c, c->soft, c->soft_off, c->vparams, npkts, c->dec, c->dec_off, c->dec_bits, ordered);
   if (ev) ZRX_CHECK(hipEventRecord(ev[4], s));
   k_descramble_crc<<<c->crc_blocks > 0 ? std::min(blocks(npkts, kCrcWaves), c->crc_blocks) : blocks(npkts, kCrcWaves),

@@ -285,12 +285,70 @@ __device__ __forceinline__ void plan_pkts(const int32_t* __restrict__ vparams, i
     if ((t & 63) == 0) atomicAdd(nrows_total, my_rows);
   }
 }
+// The mixed batch's rows (k_pkt_plan's comment): packets keyed by (rate, segment length)
+// with segment length Lm, counted and scattered in LDS (hist: kOrderPerThread x 1024 words,
+// zeroed; *rtotal zeroed), then expanded onto rows by a block scan.  1024 threads.
+__device__ __forceinline__ void plan_rows_mixed(const int32_t* __restrict__ vparams, int npkts, uint32_t Lm,
+                                                int2* __restrict__ rows, int32_t* __restrict__ nrows,
+                                                uint8_t* __restrict__ segs, int32_t* __restrict__ order,
+                                                int32_t* __restrict__ out_bits, int ncu, int rows_cap, uint32_t* hist,
+                                                uint32_t* rtotal) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  plan_pkts<false>(vparams, npkts, Lm, hist, order, segs, out_bits, rtotal);
+  __syncthreads();
+  if (ZRX_PLAN_CUT <= 3) return;
+  const uint32_t npk = order_hist_scan(hist);          // packets with rows
+  __syncthreads();
+  plan_pkts<true>(vparams, npkts, Lm, hist, order, segs, out_bits, nullptr);
+  __syncthreads();                                     // order[] and segs[] written by the block
+  if (ZRX_PLAN_CUT <= 5) return;
+  // Expand: the segments of the packet at sorted position i are rows prefix(i) .. +nseg - 1
+  // (consecutive, so a wave holds segments of one or two packets of similar length), placed
+  // snake over the CUs.  Thread t takes positions 16t .. 16t + 15 of each round.
+  const uint32_t total = *rtotal, nfull = total >> 4;
+  const uint32_t ncu2 = (uint32_t)max(ncu, 2), ncu_rcp = 0xFFFFFFFFu / ncu2 + 1u;
+  __shared__ uint32_t esum[16];
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < npk; base += 1024u * kScanPer) {
+    int32_t pk[kScanPer];
+    uint32_t ns[kScanPer], sum = 0;
+#pragma unroll
+    for (int i = 0; i < kScanPer; i++) {
+      const uint32_t pos = base + kScanPer * (uint32_t)t + i;
+      pk[i] = pos < npk ? order[pos] : -1;
+    }
+#pragma unroll
+    for (int i = 0; i < kScanPer; i++) { ns[i] = pk[i] >= 0 ? segs[pk[i]] : 0u; sum += ns[i]; }
+    const uint32_t inc = wave_incl_scan(sum);
+    if (lane == 63) esum[wv] = inc;
+    __syncthreads();
+    uint32_t ex = carry + inc - sum, rnd = 0;
+    for (int w = 0; w < 16; w++) { ex += w < wv ? esum[w] : 0u; rnd += esum[w]; }
+#pragma unroll
+    for (int i = 0; i < kScanPer; i++) {
+      for (uint32_t k = 0; k < ns[i]; k++) {
+        const uint32_t at = v3::order_place(ex + k, nfull, ncu2, ncu_rcp);
+        if (at < (uint32_t)rows_cap) rows[at] = make_int2(pk[i], (int)(k | (ns[i] << 8)));   // (always: the plan's row bound)
+      }
+      ex += ns[i];
+    }
+    carry += rnd;
+    __syncthreads();                                   // esum is rewritten by the next round
+  }
+  if (t == 0) {
+    nrows[v3::kPlanRows] = (int32_t)min(total, (uint32_t)rows_cap);
+    nrows[v3::kPlanFixes] = 0;                         // counted by the seam pass
+    nrows[v3::kPlanUniform] = 0;
+    nrows[v3::kPlanNcu] = (int32_t)ncu2;
+  }
+}
+
 __global__ __launch_bounds__(1024) void k_pkt_plan(const int32_t* __restrict__ vparams, int npkts,
                                                    int64_t* __restrict__ off, int32_t* __restrict__ dsym,
                                                    int32_t* __restrict__ wave_p0, int2* __restrict__ rows,
                                                    int32_t* __restrict__ nrows, uint8_t* __restrict__ segs,
                                                    int32_t* __restrict__ order, int32_t* __restrict__ out_bits, int ncu,
-                                                   int rows_cap) {
+                                                   int rows_cap, int split, int32_t* __restrict__ mixed_hint) {
   __shared__ uint2 wtab[kScanPer * 16];                // (chunk i, wave w) totals, then offsets
   __shared__ uint2 round_total;
   __shared__ uint32_t hist[kOrderPerThread * 1024];
@@ -371,6 +429,7 @@ __global__ __launch_bounds__(1024) void k_pkt_plan(const int32_t* __restrict__ v
   // short of four waves per SIMD stays whole)
   const uint32_t Lb = L + L / 8u;                       // (uniform batch)
   const uint32_t Lm = max(L * v3::kSegMixNum / 8u, v3::kMinSeg);   // (mixed batch)
+  if (t == 0 && mixed_hint) *mixed_hint = uniform ? 0 : 1;   // (host-mapped: the next call's split choice)
   if (uniform) {                                       // no sort: k_viterbi3 derives each row's segment
     if (t == 0) {
       const uint32_t E0 = q0.x > (1 << 21) ? 0xFFFFFFFFu : (uint32_t)q0.x * 8u + 6u;
@@ -382,54 +441,28 @@ __global__ __launch_bounds__(1024) void k_pkt_plan(const int32_t* __restrict__ v
     }
     return;
   }
-  if (ZRX_PLAN_CUT <= 2) return;
-  plan_pkts<false>(vparams, npkts, Lm, hist, order, segs, out_bits, &rtotal);
-  __syncthreads();
-  if (ZRX_PLAN_CUT <= 3) return;
-  const uint32_t npk = order_hist_scan(hist);          // packets with rows
-  __syncthreads();
-  plan_pkts<true>(vparams, npkts, Lm, hist, order, segs, out_bits, nullptr);
-  __syncthreads();                                     // order[] and segs[] written by the block
-  if (ZRX_PLAN_CUT <= 5) return;
-  // Expand: the segments of the packet at sorted position i are rows prefix(i) .. +nseg - 1
-  // (consecutive, so a wave holds segments of one or two packets of similar length), placed
-  // snake over the CUs.  Thread t takes positions 16t .. 16t + 15 of each round.
-  const uint32_t total = rtotal, nfull = total >> 4;
-  const uint32_t ncu2 = (uint32_t)max(ncu, 2), ncu_rcp = 0xFFFFFFFFu / ncu2 + 1u;
-  __shared__ uint32_t esum[16];
-  uint32_t carry = 0;
-  for (uint32_t base = 0; base < npk; base += 1024u * kScanPer) {
-    int32_t pk[kScanPer];
-    uint32_t ns[kScanPer], sum = 0;
-#pragma unroll
-    for (int i = 0; i < kScanPer; i++) {
-      const uint32_t pos = base + kScanPer * (uint32_t)t + i;
-      pk[i] = pos < npk ? order[pos] : -1;
-    }
-#pragma unroll
-    for (int i = 0; i < kScanPer; i++) { ns[i] = pk[i] >= 0 ? segs[pk[i]] : 0u; sum += ns[i]; }
-    const uint32_t inc = wave_incl_scan(sum);
-    if (lane == 63) esum[wv] = inc;
-    __syncthreads();
-    uint32_t ex = carry + inc - sum, rnd = 0;
-    for (int w = 0; w < 16; w++) { ex += w < wv ? esum[w] : 0u; rnd += esum[w]; }
-#pragma unroll
-    for (int i = 0; i < kScanPer; i++) {
-      for (uint32_t k = 0; k < ns[i]; k++) {
-        const uint32_t at = v3::order_place(ex + k, nfull, ncu2, ncu_rcp);
-        if (at < (uint32_t)rows_cap) rows[at] = make_int2(pk[i], (int)(k | (ns[i] << 8)));   // (always: the plan's row bound)
-      }
-      ex += ns[i];
-    }
-    carry += rnd;
-    __syncthreads();                                   // esum is rewritten by the next round
+  if (split) {                                         // k_pkt_rows sorts and expands, on a side stream
+    if (t == 0) { nrows[v3::kPlanUniform] = 0; nrows[v3::kPlanSegLen] = (int32_t)Lm; }
+    return;
   }
-  if (t == 0) {
-    nrows[v3::kPlanRows] = (int32_t)min(total, (uint32_t)rows_cap);
-    nrows[v3::kPlanFixes] = 0;                         // counted by the seam pass
-    nrows[v3::kPlanUniform] = 0;
-    nrows[v3::kPlanNcu] = (int32_t)ncu2;
-  }
+  plan_rows_mixed(vparams, npkts, Lm, rows, nrows, segs, order, out_bits, ncu, rows_cap, hist, &rtotal);
+}
+
+// The second half of a split plan (rx chain): the mixed batch's sort and row expansion, on a
+// side stream while k_data_fft runs (it needs only the first half's offsets).  Nothing to do
+// for a uniform batch, whose header k_pkt_plan wrote.
+__global__ __launch_bounds__(1024) void k_pkt_rows(const int32_t* __restrict__ vparams, int npkts,
+                                                   int2* __restrict__ rows, int32_t* __restrict__ nrows,
+                                                   uint8_t* __restrict__ segs, int32_t* __restrict__ order,
+                                                   int32_t* __restrict__ out_bits, int ncu, int rows_cap) {
+  if (nrows[v3::kPlanUniform] != 0) return;
+  __shared__ uint32_t hist[kOrderPerThread * 1024];
+  __shared__ uint32_t rtotal;
+  const uint32_t Lm = (uint32_t)nrows[v3::kPlanSegLen];
+  for (int i = threadIdx.x; i < kOrderPerThread * 1024; i += 1024) hist[i] = 0;
+  if (threadIdx.x == 0) rtotal = 0;
+  __syncthreads();
+  plan_rows_mixed(vparams, npkts, Lm, rows, nrows, segs, order, out_bits, ncu, rows_cap, hist, &rtotal);
 }
 
 constexpr int kDataFftBlocks = 2048;  // k_data_fft grid cap: 8192 waves, 32 per CU, looping
