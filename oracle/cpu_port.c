@@ -379,6 +379,50 @@ static void* pworker(void* p) {
 }
 static void init_all(void) { init_tables(); init_vit_tables(); g_avx = have_avx512(); }
 
+/* Same contract as zo_viterbi_batch (init + decode of all soft values per packet, depth
+   256), packet-parallel with dynamic claiming. */
+typedef struct {
+  const int8_t* soft; const int64_t* soft_off; const int32_t* soft_len; const int32_t* frame_len;
+  const int16_t* code_rate; uint8_t* out; const int64_t* out_off; int npkts; int* next;
+} vjob_t;
+static void* vworker(void* p) {
+  vjob_t* j = (vjob_t*)p;
+  pv_t v; memset(&v, 0, sizeof(v));
+  v.cap = 40000 + 8;
+  v.surv = (uint64_t*)calloc(v.cap, sizeof(uint64_t));
+  zo_vit zv; memset(&zv, 0, sizeof(zv));
+  for (int i; (i = __atomic_fetch_add(j->next, 1, __ATOMIC_RELAXED)) < j->npkts;) {
+    const int8_t* s = j->soft + j->soft_off[i];
+    uint8_t* o = j->out + j->out_off[i];
+    if (g_avx) {
+      for (int q = 0; q < 64; q++) v.m[q] = q ? 48 : 0;
+      v.tr = v.ob = 0; v.frame_len = (uint32_t)j->frame_len[i]; v.cr = (uint32_t)j->code_rate[i];
+      v.surv[0] = 0;
+      pv_decode_avx512(&v, s, j->soft_len[i], o);
+    } else {
+      zo_vit_init(&zv, j->frame_len[i], j->code_rate[i], 256);
+      zo_vit_decode(&zv, s, j->soft_len[i], o);
+    }
+  }
+  free(v.surv);
+  zo_vit_free(&zv);
+  return 0;
+}
+int zp_viterbi_batch(const int8_t* soft, const int64_t* soft_off, const int32_t* soft_len,
+                     const int32_t* frame_len, const int16_t* code_rate, int npkts,
+                     uint8_t* out, const int64_t* out_off, int nthreads) {
+  pthread_once(&g_once, init_all);
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  pthread_t th[256];
+  int next = 0;
+  vjob_t j = {soft, soft_off, soft_len, frame_len, code_rate, out, out_off, npkts, &next};
+  for (int t = 1; t < nthreads; t++) pthread_create(&th[t], 0, vworker, &j);
+  vworker(&j);
+  for (int t = 1; t < nthreads; t++) pthread_join(th[t], 0);
+  return g_avx;
+}
+
 /* n FFT64s by the port's own FFT (tests/test_cpu_port.py compares them with the oracle's) */
 int zp_fft64(const zo_c16* in, zo_c16* out, int n) {
   pthread_once(&g_once, init_all);

@@ -193,14 +193,16 @@ def vit_lut(which, soft, k, j):
     return lib().zo_vit_lut(which, soft, k, j)
 
 
-def viterbi_batch(soft, soft_off, soft_len, frame_len, code_rate, out_off, out_size, nthreads=1):
+def viterbi_batch(soft, soft_off, soft_len, frame_len, code_rate, out_off, out_size, nthreads=1, fast=False):
+    """fast: the CPU port's AVX-512 brick loop (zp_viterbi_batch, bench.py's config-2
+    cpu_baseline), identical output (tests/test_cpu_port.py)."""
     soft = np.ascontiguousarray(soft, np.int8)
     out = np.zeros(out_size, np.uint8)
     args = [np.ascontiguousarray(a, t) for a, t in
             ((soft_off, np.int64), (soft_len, np.int32), (frame_len, np.int32),
              (code_rate, np.int16), (out_off, np.int64))]
-    lib().zo_viterbi_batch(_p(soft), _p(args[0]), _p(args[1]), _p(args[2]), _p(args[3]),
-                           len(args[0]), _p(out), _p(args[4]), nthreads)
+    fn = lib().zp_viterbi_batch if fast else lib().zo_viterbi_batch
+    fn(_p(soft), _p(args[0]), _p(args[1]), _p(args[2]), _p(args[3]), len(args[0]), _p(out), _p(args[4]), nthreads)
     return out
 
 

@@ -79,6 +79,9 @@ int zo_rx_packet_time(const zo_c16* sym, int nsym, uint8_t* payload, zo_rx_resul
 /* The same chain by the fast CPU port (cpu_port.c; bench.py's cpu_baseline only), identical
    results to zo_rx_batch_time; returns 1 when its AVX-512 Viterbi ran. */
 int zp_fft64(const zo_c16* in, zo_c16* out, int n);
+int zp_viterbi_batch(const int8_t* soft, const int64_t* soft_off, const int32_t* soft_len,
+                     const int32_t* frame_len, const int16_t* code_rate, int npkts,
+                     uint8_t* out, const int64_t* out_off, int nthreads);
 int zp_rx_batch_time(const zo_c16* sym, const int64_t* sym_off, const int32_t* nsym, int npkts,
                      uint8_t* payload, int payload_stride, zo_rx_result* res, int nthreads);
 /* same, fed frequency-domain data subcarriers (48 per symbol, GetData order) */

@@ -49,3 +49,26 @@ def test_port_fft64_vs_oracle(oracle):
     L.zp_fft64(oracle._p(x), oracle._p(got), x.shape[0])
     want = oracle.fft64(x.reshape(-1, 64, 2))
     assert (got == want.reshape(got.shape)).all()
+
+
+def test_port_viterbi_batch_vs_oracle(oracle):
+    """zp_viterbi_batch (config 2's CPU baseline) equals zo_viterbi_batch: all rates, lengths
+    1..4095 B, clean to pure-noise soft values, truncated input."""
+    from tests.golden import synth
+    rng = np.random.default_rng(31)
+    softs, fl, cr = [], [], []
+    for i in range(60):
+        c = i % 3
+        f = int(rng.choice([1, 3, 100, 1500, 4095])) if i % 5 else int(rng.integers(1, 2048))
+        s = synth.viterbi_soft(c, f, int(rng.integers(-1, 6)), seed=400 + i)
+        if i % 7 == 6:
+            s = s[: s.size // 2 // 12 * 12]
+        softs.append(s); fl.append(f); cr.append(c)
+    sl = np.array([s.size for s in softs], np.int64)
+    so = np.cumsum(sl) - sl
+    oo = np.cumsum(np.array(fl, np.int64) + 16) - (np.array(fl, np.int64) + 16)
+    size = int(oo[-1] + fl[-1] + 16)
+    args = (np.concatenate(softs), so, sl, fl, cr, oo, size)
+    a = oracle.viterbi_batch(*args, nthreads=4)
+    b = oracle.viterbi_batch(*args, nthreads=4, fast=True)
+    assert (a == b).all()
