@@ -8,6 +8,7 @@
 #include "../../ziria_amd/csrc/zrx_kernels.hip"
 using namespace zrx;
 
+static int g_split = 0;   // argv[1] = 1: k_pkt_plan as the rx chain launches it (mixed rows left to k_pkt_rows)
 static void run(const char* name, const std::vector<int32_t>& vp, int npkts, bool chain) {
   int32_t *d_vp, *d_nrows, *d_order, *d_bits, *d_dsym, *d_w;
   int64_t* d_off;
@@ -15,13 +16,13 @@ static void run(const char* name, const std::vector<int32_t>& vp, int npkts, boo
   uint8_t* d_segs;
   hipMalloc(&d_vp, vp.size() * 4);
   hipMemcpy(d_vp, vp.data(), vp.size() * 4, hipMemcpyHostToDevice);
-  hipMalloc(&d_nrows, 16); hipMalloc(&d_order, npkts * 4); hipMalloc(&d_bits, npkts * 4);
+  hipMalloc(&d_nrows, 32); hipMalloc(&d_order, npkts * 4); hipMalloc(&d_bits, npkts * 4);
   hipMalloc(&d_dsym, npkts * 4 + 8); hipMalloc(&d_w, (size_t)npkts * 1400 / 64 * 4 + 64);
   hipMalloc(&d_off, npkts * 8); hipMalloc(&d_rows, (size_t)(npkts + 16384) * 8); hipMalloc(&d_segs, npkts);
   hipEvent_t a, b;
   hipEventCreate(&a); hipEventCreate(&b);
   auto launch = [&]() {
-    k_pkt_plan<<<1, 1024>>>(d_vp, npkts, chain ? d_off : nullptr, d_dsym, d_w, d_rows, d_nrows, d_segs, d_order, d_bits, 256, npkts + 16384, 0, nullptr);
+    k_pkt_plan<<<1, 1024>>>(d_vp, npkts, chain ? d_off : nullptr, d_dsym, d_w, d_rows, d_nrows, d_segs, d_order, d_bits, 256, npkts + 16384, g_split, nullptr);
   };
   for (int i = 0; i < 5; i++) launch();
   hipEventRecord(a);
@@ -32,10 +33,11 @@ static void run(const char* name, const std::vector<int32_t>& vp, int npkts, boo
   hipEventElapsedTime(&ms, a, b);
   int nr[2];
   hipMemcpy(nr, d_nrows, 8, hipMemcpyDeviceToHost);
-  std::printf("cut %d %-8s %6d pkts: %7.2f us  rows %d\n", ZRX_PLAN_CUT, name, npkts, ms * 1000 / 50, nr[0]);
+  std::printf("split %d cut %d %-8s %6d pkts: %7.2f us  rows %d\n", g_split, ZRX_PLAN_CUT, name, npkts, ms * 1000 / 50, nr[0]);
 }
 
-int main() {
+int main(int argc, char** argv) {
+  g_split = argc > 1 ? std::atoi(argv[1]) : 0;
   const int n = 16384;
   std::vector<int32_t> c3(4 * n), c5(4 * n), c2(4 * 4096);
   for (int i = 0; i < n; i++) { c3[4 * i] = 1506; c3[4 * i + 1] = 2; c3[4 * i + 2] = 56 * 288; c3[4 * i + 3] = 3; }
