@@ -1,0 +1,66 @@
+"""Packet-for-packet parity at BASELINE's full batch sizes: every one of 16384 packets of a
+config-3 batch (clean, and at the noise edge where CRCs fail), and of a 16384-packet config-5
+batch of distinct mixed-MCS packets, decoded by the HIP chain, against the same batch decoded
+on the host by oracle/cpu_port.c.  The port is the oracle's chain written for speed, identical
+to the oracle (tests/test_cpu_port.py), so it can check a whole batch in about a second; the
+oracle itself checks the smaller GPU cases in test_gpu_parity.py."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+from ziria_amd import txgen  # noqa: E402
+from ziria_amd.engine import RxEngine  # noqa: E402
+
+
+def _threads():
+    try:
+        return max(1, min(16, len(os.sched_getaffinity(0))))
+    except AttributeError:
+        return 8
+
+
+def _check(oracle, b):
+    n = b["sym_off"].numel()
+    e = RxEngine(0)
+    try:
+        e.reserve(n, b["max_nsym"])
+        pay, info = e.rx(b["sym"], b["sym_off"], b["nsym"], b["max_nsym"])
+        torch.cuda.synchronize()
+        pay, info = pay.cpu().numpy(), info.cpu().numpy()
+    finally:
+        e.close()
+    opay, res = oracle.rx_batch_time_fast(b["sym"].cpu().numpy(), b["sym_off"].cpu().numpy(),
+                                          b["nsym"].cpu().numpy(), nthreads=_threads())
+    hdr = np.array([(r["modulation"], r["coding"], r["len"], r["err"]) for r in res], np.int32)
+    crc = np.array([r["crc_ok"] for r in res], np.int32)
+    assert (info[:, :4] == hdr).all(), np.nonzero((info[:, :4] != hdr).any(1))[0][:10]
+    assert (info[:, 4] == crc).all(), np.nonzero(info[:, 4] != crc)[0][:10]
+    plen = np.maximum(hdr[:, 2] - 4, 0)
+    bad = [i for i in range(n) if not hdr[i, 3] and not (pay[i, :plen[i]] == opay[i, :plen[i]]).all()]
+    assert not bad, bad[:10]
+    return crc
+
+
+def test_fullsize_config3_vs_port(oracle):
+    b = txgen.make_batch(16384, seed=0x5EED, sigma=4.0, device="cuda")
+    crc = _check(oracle, b)
+    assert crc.all()
+
+
+def test_fullsize_config3_noise_edge_vs_port(oracle):
+    b = txgen.make_batch(16384, seed=58, sigma=58.0, device="cuda")
+    crc = _check(oracle, b)
+    assert 0 < crc.sum() < crc.size                        # CRC failures do occur here
+
+
+def test_fullsize_config5_vs_port(oracle):
+    m = txgen.make_mixed_fast(16384, min_len=64, max_len=4095, sigma=3.0, seed=0xC5C6, device="cuda")
+    crc = _check(oracle, m)
+    assert crc.sum() > 7000
