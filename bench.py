@@ -69,6 +69,9 @@ def main():
     ap.add_argument("--payload", type=int, default=1500)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall time budget of the CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--pipeline", type=int, default=2, choices=[1, 2],
+                    help="batches in flight: 2 = two engines (own workspace and stream) take the steps in "
+                         "turn, as a streaming receiver would, so one batch's tail overlaps the next one's head")
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 5])
     ap.add_argument("--tx", action="store_true",
                     help="TX chain (transmitter() at 40 MHz, SURVEY §8f row 4) on config-3 packets")
@@ -97,29 +100,57 @@ def main():
     # builds and decodes its contiguous shard, rank 0 checks every gathered packet.
     total = args.total if args.total else args.npkts * world
     sigma = 2.0 if args.eq else 4.0
-    eng = RxEngine(local)
-    state = {}
+    # args.pipeline engines, each with its own workspace and stream, take the steps in turn;
+    # every step is still one whole pass of the chain over the shard
+    engs = [RxEngine(local) for _ in range(args.pipeline)]
+    streams = [torch.cuda.Stream(dev) for _ in range(args.pipeline)]
+    eng = engs[0]
+    state = {"k": 0}
 
     def make_shard(lo, hi):
         b = txgen.make_batch_range(lo, hi, mod=3, coding=2, payload_len=args.payload, sigma=sigma, seed=0x5EED,
                                    device=dev, channel=args.eq)
         n, S = hi - lo, b["max_nsym"]
-        eng.reserve(max(n, 1), S)
-        b["out_payload"] = torch.zeros((n, 4096), dtype=torch.uint8, device=dev)
-        b["out_info"] = torch.zeros((n, 8), dtype=torch.int32, device=dev)
+        for e in engs:
+            e.reserve(max(n, 1), S)
+        b["outs"] = [(torch.zeros((n, 4096), dtype=torch.uint8, device=dev),
+                      torch.zeros((n, 8), dtype=torch.int32, device=dev)) for _ in engs]
+        b["out_payload"], b["out_info"] = b["outs"][0]
         state["b"] = b
         return b
 
+    def run_on(j, b):
+        with torch.cuda.stream(streams[j]):
+            engs[j].rx(b["sym"], b["sym_off"], b["nsym"], b["max_nsym"], b["outs"][j][0], b["outs"][j][1],
+                       chan=b.get("chan"))
+
     def step(b):
-        eng.rx(b["sym"], b["sym_off"], b["nsym"], b["max_nsym"], b["out_payload"], b["out_info"], chan=b.get("chan"))
+        j = state["k"] % len(engs)
+        state["k"] += 1
+        run_on(j, b)
+
+    # stage times: a separate instrumented pass of engine 0 alone, after the warmup and before
+    # the timed steps (the pipelined steps overlap, so their per-stream event spans would include
+    # the other batch; the timers' own event records stay out of the timed region)
+    def instrumented(on):
+        if not on:
+            return
+        eng.enable_timing(True)
+        for _ in range(max(3, min(args.steps, 10))):
+            run_on(0, state["b"])
+        torch.cuda.synchronize(dev)
+        state["stage"] = eng.stage_ms()
+        eng.enable_timing(False)
 
     res = node.run_sharded(total, make_shard, step, lambda b: (b["out_payload"], b["out_info"]),
                            lambda lo, hi: txgen.payloads_range(lo, hi, args.payload, seed=0x5EED),
                            args.steps, args.warmup, args.payload, device=dev, crc_ok_only=args.eq,
-                           on_timed=lambda on: eng.enable_timing(on) if on else None)
-    stage = eng.stage_ms()                        # averages over the K timed steps
-    eng.enable_timing(False)
+                           on_timed=instrumented)
     b = state["b"]
+    stage = state["stage"]
+    torch.cuda.synchronize(dev)
+    outs_equal = all(bool((o[0] == b["outs"][0][0]).all()) and bool((o[1] == b["outs"][0][1]).all())
+                     for o in b["outs"][1:])
     n, S = res["hi"] - res["lo"], b["max_nsym"]
     elapsed = res["elapsed"]
 
@@ -159,12 +190,15 @@ def main():
                                    "time-domain input resident in HBM"
                                    + (", FFT >>> ChannelEqualization >>> PilotTrack >>> GetData" if args.eq else ""),
                        "packets_total": total, "packets_per_gpu": n, "payload_bytes": args.payload,
-                       "symbols_per_packet": S, "parallelism": f"packet-sharded x{world}"},
+                       "symbols_per_packet": S, "parallelism": f"packet-sharded x{world}",
+                       "pipeline": f"{len(engs)} batches in flight (engines on separate streams, steps in turn)"},
             "bit_exact_check": {"crc_pass": res["ok"], "packets": res["packets"],
                                 "payload_match": res["payload_match"],
                                 "mismatched_packets": res["mismatched_packets"],
+                                "pipeline_outputs_equal": outs_equal,
                                 "checked_on": "rank 0, every gathered packet vs its transmitted payload"},
             "stage_ms": {k: round(v, 4) for k, v in stage.items()},
+            "stage_ms_from": "engine 0 alone, HIP events, after the warmup and before the timed steps",
             "roofline": {"kernel": "k_viterbi3 (data Viterbi)", "bound": "valu",
                          "achieved": round(achieved_tops, 3), "peak": round(VALU_PEAK_TOPS, 1),
                          "unit": "Tops/s", "frac": round(achieved_tops / VALU_PEAK_TOPS, 4),
@@ -268,18 +302,37 @@ def bench_mixed(args):
     m = txgen.make_mixed_fast(n, min_len=64, max_len=4095, sigma=3.0, seed=0x3C5, device=dev)
     gen_s = time.perf_counter() - tg
     S = m["max_nsym"]
-    eng = RxEngine(0)
-    eng.reserve(n, S)
-    payload = torch.zeros((n, 4096), dtype=torch.uint8, device=dev)
-    info = torch.zeros((n, 8), dtype=torch.int32, device=dev)
-    step = lambda: eng.rx(m["sym"], m["sym_off"], m["nsym"], S, payload, info)
+    # args.pipeline engines (own workspace and stream) take the steps in turn, as in main()
+    engs = [RxEngine(0) for _ in range(args.pipeline)]
+    streams = [torch.cuda.Stream(dev) for _ in engs]
+    outs = []
+    for e in engs:
+        e.reserve(n, S)
+        outs.append((torch.zeros((n, 4096), dtype=torch.uint8, device=dev),
+                     torch.zeros((n, 8), dtype=torch.int32, device=dev)))
+    eng = engs[0]
+    payload, info = outs[0]
+    k = {"i": 0}
+
+    def run_on(j):
+        with torch.cuda.stream(streams[j]):
+            engs[j].rx(m["sym"], m["sym_off"], m["nsym"], S, outs[j][0], outs[j][1])
+
+    def step():
+        run_on(k["i"] % len(engs))
+        k["i"] += 1
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    eng.enable_timing(True)                              # timed steps only
-    elapsed = _timed(step, args.steps, 0)
+    eng.enable_timing(True)                              # stage times: engine 0 alone, before the timed steps
+    for _ in range(max(3, min(args.steps, 10))):
+        run_on(0)
+    torch.cuda.synchronize()
     stage = eng.stage_ms()
     eng.enable_timing(False)
+    elapsed = _timed(step, args.steps, 0)
+    outs_equal = all(bool((o[0] == payload).all()) and bool((o[1] == info).all()) for o in outs[1:])
     inf = info.cpu().numpy()
     pay = payload.cpu().numpy()
     ok = inf[:, 4] == 1
@@ -304,7 +357,9 @@ def bench_mixed(args):
                 f"generated in {gen_s:.1f} s)",
         "config": {"workload": f"config5: {n} packets, {S} symbols max, {int(m['nsym'].sum())} symbols"},
         "bit_exact_check": {"crc_pass": int(ok.sum()), "expected_crc_pass": expect_ok, "payload_match": good,
-                            "oracle_sample": sample, "oracle_sample_match": bool(oracle_match)},
+                            "oracle_sample": sample, "oracle_sample_match": bool(oracle_match),
+                            "pipeline_outputs_equal": outs_equal},
+        "pipeline": f"{len(engs)} batches in flight (engines on separate streams, steps in turn)",
         "stage_ms": {k: round(v, 4) for k, v in stage.items()},
         "cpu_baseline": cpu,
     }), flush=True)

@@ -115,7 +115,8 @@ def run_sharded(total, make_shard, step, outputs, expected, steps, warmup, paylo
     info int32 [n, 8]) of the last step; expected(lo, hi) -> uint8 numpy [hi-lo, L], the
     transmitted payloads (L = payload_len bytes each), which rank 0 uses to check every
     gathered packet.
-    on_timed(True/False) is called right before / after the timed steps (stage timers).
+    on_timed(True) is called after the warmup, before the barrier that opens the timed region
+    (bench.py runs its instrumented stage-timer pass there), on_timed(False) after it closes.
 
     Timing: `warmup` untimed steps, then barrier + device sync, `steps` timed steps, device
     sync + barrier, and the slowest rank's time.  Returns on every rank a dict with the
@@ -126,10 +127,11 @@ def run_sharded(total, make_shard, step, outputs, expected, steps, warmup, paylo
     for _ in range(warmup):
         step(shard)
     _sync(device)
-    barrier(device)
-    _sync(device)
     if on_timed:
         on_timed(True)
+    _sync(device)
+    barrier(device)
+    _sync(device)
     t0 = time.perf_counter()
     for _ in range(steps):
         step(shard)
