@@ -1,18 +1,23 @@
 /*
  * ziria_rx.h — C-ABI of the MI355X (gfx950) 802.11a RX decode engine, libziria_rx.so.
  *
- * Part 1 re-exports the reference's own external bricks with identical C signatures and
- * per-call semantics, so Ziria-generated C (wplc output, which calls `__ext_<name>` with
- * every array argument expanded to (pointer, length), src/Codegen/CgFun.hs:287-316 and
- * src/Codegen/CgCall.hs:72-130) links against this library unchanged.  Each call runs
- * on the GPU (batch of one); there is no CPU compute path in this library.
+ * Part 1 re-exports the reference's own external bricks with identical signatures and
+ * per-call semantics.  wplc emits every `fun external f` as a prototype `__ext_f(...)` with
+ * each array argument expanded to (pointer, length) (src/Codegen/CgFun.hs:287-316,
+ * src/Codegen/CgCall.hs:72-130) into a test.cpp that the reference builds with g++
+ * (csrc/Makefile:92-96), i.e. with C++ linkage and the reference's types (num8 = char,
+ * int16 = short, int32 = int; csrc/numerics.h:64-69, csrc/types.h:32-33).  So the library
+ * exports each external twice: with those C++ (mangled) names, which a C++ includer of this
+ * header sees and a wplc-compiled program links against unchanged, and with C linkage
+ * (unmangled), which a C includer and ctypes see.  The per-call externals run on the host
+ * CPU ("a CPU path, with the GPU used only if batched").
  *
- * Part 2 adds batched counterparts over host arrays.  They use only arrays and scalars, so
- * they can be declared in a .blk file as `fun external` (INTEGRATION.md shows the
- * declarations).
+ * Part 2 adds batched counterparts over host arrays, run on the GPU.  They use only arrays
+ * and scalars, so they can be declared in a .blk file as `fun external` (INTEGRATION.md
+ * shows the declarations); like Part 1 they are exported with both linkages.
  *
  * Part 3 is the throughput API over device-resident buffers (HBM), asynchronous on a
- * caller-provided HIP stream; this is what bench.py and the Python engine drive.
+ * caller-provided HIP stream; this is what bench.py and the Python engine drive.  C linkage.
  *
  * All buffers are caller-owned.  Status-returning functions return ZRX_OK (0) or a
  * negative ZRX_E* code; the reference's own externals keep their reference return values.
@@ -21,20 +26,22 @@
 #define ZIRIA_RX_H
 #include <stdint.h>
 
-#ifdef __cplusplus
-extern "C" {
-#endif
-
 /* csrc/numerics.h:113-116 */
 struct complex16 { int16_t re; int16_t im; };
+
+/* Parts 1 and 2: C++ linkage for C++ includers (the names wplc output links against); C
+ * linkage for C includers and inside the library's C-linkage translation units. */
+#if defined(__cplusplus) && defined(ZRX_C_LINKAGE_EXTERNALS)
+extern "C" {
+#endif
 
 /* ================================================================ Part 1: reference bricks */
 
 /* Replaces __ext_sora_fft (reference csrc/sora_ext_lib.cpp:2672-2812, declared
- * lib/externals.blk:201-202): FFTSafe<nFFTSize> on the GPU for every size the reference
- * dispatches (16, 32, ..., 2048 and the LTE sizes 12 .. 1200, listed at zrx_fft_dev); any
- * other size prints the reference's error message and leaves `out` untouched, as the
- * reference does (:2808-2810). */
+ * lib/externals.blk:201-202): FFTSafe<nFFTSize> on the host CPU for every size the
+ * reference dispatches (16, 32, ..., 2048 and the LTE sizes 12 .. 1200, listed at
+ * zrx_fft_dev, the batched GPU counterpart); any other size prints the reference's error
+ * message and leaves `out` untouched, as the reference does (:2808-2810).  in/out may alias. */
 void __ext_sora_fft(struct complex16* out, int nFFTSize, struct complex16* in, int unused1);
 
 /* Replaces __ext_sora_fft_dynamic (sora_ext_lib.cpp:2816-2820, externals.blk:205-206). */
@@ -42,13 +49,17 @@ void __ext_sora_fft_dynamic(struct complex16* out, int unused2, int16_t nFFTSize
                             struct complex16* in, int unused1);
 
 /* Replaces __ext_viterbi_brick_init_fast (csrc/sora_ext_viterbi.cpp:48-63,
- * externals.blk:215).  Resets the (single, global, non-reentrant) streaming decoder. */
+ * externals.blk:215).  Resets the (single, global, non-reentrant) streaming decoder; like
+ * the reference it keeps frame_len as an unsigned 16-bit value. */
 int __ext_viterbi_brick_init_fast(int32_t frame_len, int16_t code_rate, int16_t depth);
 
 /* Replaces __ext_viterbi_brick_decode_fast (sora_ext_viterbi.cpp:66-153,
- * externals.blk:216): consumes len1 soft values (whole groups), appends the decoded bytes
- * to `bit` (LSB-first bits), returns the number of bits appended by this call. */
-int16_t __ext_viterbi_brick_decode_fast(int8_t* intInput, int len1, unsigned char* bit, int len2);
+ * externals.blk:216): consumes len1 soft values (whole groups of 2/3/4 for rate 1/2, 2/3,
+ * 3/4), runs the brick's normalize and traceback schedule, writes the bytes this call
+ * decodes to bit[0..] (LSB-first bits) and returns their bit count.  Like the reference it
+ * does not bound the writes by len2.  The trellis holds 40000 columns (TRELLIS_MAX, :39):
+ * groups beyond it are not consumed (the reference writes past its buffer). */
+int16_t __ext_viterbi_brick_decode_fast(char* intInput, int len1, unsigned char* bit, int len2);
 
 /* Replaces __ext_viterbiSig11a_brick_init_fast (sora_ext_viterbi.cpp:158-173). */
 int __ext_viterbiSig11a_brick_init_fast(int32_t frame_len, int16_t code_rate, int16_t depth);
@@ -56,7 +67,7 @@ int __ext_viterbiSig11a_brick_init_fast(int32_t frame_len, int16_t code_rate, in
 /* Replaces __ext_viterbiSig11a_brick_decode_fast (sora_ext_viterbi.cpp:176-194,
  * externals.blk:217): 48 soft values -> 24 PLCP bits; like the reference it then shifts
  * the 32-bit word at `bit` right by 6 (so `bit` must hold 4 bytes).  Returns 0. */
-int16_t __ext_viterbiSig11a_brick_decode_fast(int8_t* intInput, int len1, unsigned char* bit, int len2);
+int16_t __ext_viterbiSig11a_brick_decode_fast(char* intInput, int len1, unsigned char* bit, int len2);
 
 /* Replaces __ext_v_shift_right_complex16 (sora_ext_lib.cpp:1979-1995, externals.blk:110). */
 int __ext_v_shift_right_complex16(struct complex16* z, int unused3, struct complex16* x, int len,
@@ -72,7 +83,7 @@ void __ext_sora_fft64_batch(struct complex16* out, int outlen, struct complex16*
  * writing its bytes at out_bits[pkt_out_off[i] ..] (byte offsets; bytes are LSB-first bit
  * arrays).  pkt_soft_off has npkts+1 entries; every per-packet soft count must be a multiple
  * of 48.  Returns the number of packets decoded, or a negative ZRX_E* code. */
-int32_t __ext_viterbi_batch_decode(int8_t* soft, int softlen, int32_t* pkt_soft_off, int n_off,
+int32_t __ext_viterbi_batch_decode(char* soft, int softlen, int32_t* pkt_soft_off, int n_off,
                                    int32_t* frame_len, int n_fl, int16_t* code_rate, int n_cr,
                                    unsigned char* out_bits, int out_len_bits,
                                    int32_t* pkt_out_off, int n_oo);
@@ -119,7 +130,14 @@ int32_t __ext_wifi_rx_stream_batch(struct complex16* samples, int nsamples, int3
 int32_t __ext_wifi_tx_batch(unsigned char* in, int inlen, int32_t* pkt_in_off, int n_off,
                             struct complex16* out, int outlen, int32_t* pkt_out_off, int n_oo);
 
+#if defined(__cplusplus) && defined(ZRX_C_LINKAGE_EXTERNALS)
+}
+#endif
+
 /* ================================================================ Part 3: device API */
+#ifdef __cplusplus
+extern "C" {
+#endif
 
 #define ZRX_OK 0
 #define ZRX_EINVAL (-1)    /* bad argument (sizes, rates, soft count not a group multiple) */

@@ -1,6 +1,7 @@
 """GPU parity: the HIP engine (through the C-ABI of libziria_rx.so) against the oracle, the
 reference's own KATs and the reference-brick golden fixtures.  Integer/byte work, so every
-comparison is bit-exact (no tolerance)."""
+comparison is bit-exact (no tolerance).  The per-call externals run on the host and are
+tested without a GPU in tests/test_percall_host.py."""
 import numpy as np
 import pytest
 
@@ -27,12 +28,6 @@ def test_library_is_native():
 
 
 # ------------------------------------------------------------------ FFT64
-def test_fft64_kat(golden):
-    k = golden["ref_kats"]
-    out = Z.sora_fft(k["fft64_kat_in"])
-    assert (out == k["fft64_kat_out"]).all()
-
-
 def test_fft64_reference_vectors(golden):
     g = golden["ref_fft64"]
     out = Z.sora_fft64_batch(g["fft_in"])
@@ -45,25 +40,6 @@ def test_fft64_device_random_vs_oracle(engine, oracle):
     x[:500] = rng.choice(np.array([-32768, 32767, -1, 0], np.int16), (500, 64, 2))
     out = engine.fft64(torch.from_numpy(x).cuda()).cpu().numpy()
     assert (out == oracle.fft64(x)).all()
-
-
-def test_fft_unsupported_size_leaves_output():
-    for n in (20, 100, 4096):
-        x = np.ones((n, 2), np.int16)
-        assert (Z.sora_fft(x) == 0).all()
-    assert (Z.sora_fft_dynamic(64, np.ones((64, 2), np.int16)) ==
-            Z.sora_fft(np.ones((64, 2), np.int16))).all()
-
-
-def test_fft_all_sizes_kat_per_call(golden):
-    """__ext_sora_fft per call on every block of tests/libs/test_fft (all 42 sizes)."""
-    g = golden["ref_fftn"]
-    off = 0
-    for n in g["sizes"]:
-        n = int(n)
-        assert (Z.sora_fft(g["kat_in"][off:off + n]) == g["kat_out"][off:off + n]).all(), n
-        assert (Z.sora_fft_dynamic(n, g["kat_in"][off:off + n]) == g["kat_out"][off:off + n]).all(), n
-        off += n
 
 
 def test_fft_all_sizes_reference_vectors(engine, golden):
@@ -92,27 +68,7 @@ def test_fft_all_sizes_random_vs_oracle(engine, oracle):
         assert (d.cpu().numpy() == exp).all(), n
 
 
-def test_v_shift_right_complex16(oracle):
-    rng = np.random.default_rng(5)
-    for n in (1, 3, 4, 5, 8, 13):
-        for sh in (0, 1, 7, 15, 16):
-            x = rng.integers(-32768, 32768, (n, 2)).astype(np.int16)
-            assert (Z.v_shift_right_complex16(x, sh) == oracle.v_shift_right_complex16(x, sh)).all()
-
-
 # ------------------------------------------------------------------ Viterbi
-def test_viterbi_kat(golden):
-    k = golden["ref_kats"]
-    Z.viterbi_brick_init_fast(100, 0, 256)
-    outs = []
-    s = k["vit_kat_soft"]
-    for i in range(0, s.size, 48):
-        nb, b = Z.viterbi_brick_decode_fast(s[i:i + 48])
-        outs.append(b)
-    bits = np.unpackbits(np.concatenate(outs), bitorder="little")
-    assert (bits == k["vit_kat_bits"]).all()
-
-
 def _vit_cases(golden):
     g = golden["ref_viterbi"]
     return g, g["vit_cases"], g["vit_soft_off"], g["vit_out_off"]
@@ -139,61 +95,6 @@ def test_viterbi_adversarial_wrap(golden):
         assert (out[:exp.size] == exp).all()
 
 
-def test_viterbi_per_call_stream(golden):
-    g, cases, so, oo = _vit_cases(golden)
-    for i, (cr, fl, noise) in enumerate(cases):
-        if fl not in (1, 3, 333) or noise not in (3, -1):
-            continue
-        Z.viterbi_brick_init_fast(int(fl), int(cr), 256)
-        s = g["vit_soft"][so[i]:so[i + 1]]
-        outs = []
-        for k in range(0, s.size, 48):
-            nb, b = Z.viterbi_brick_decode_fast(s[k:k + 48])
-            assert nb == 8 * b.size
-            outs.append(b)
-        got = np.concatenate(outs)
-        assert (got == g["vit_out"][oo[i]:oo[i + 1]]).all(), f"case {(cr, fl, noise)}"
-
-
-def test_viterbi_per_call_depths_vs_oracle(oracle):
-    """Per-call externals with depths other than 256 and call sizes other than 48, call by
-    call against the oracle (itself pinned on these cases by test_oracle_vs_ref.py).  Most
-    calls emit nothing and are queued on the host; the others run the queue on the GPU."""
-    from tests.golden import synth
-    from tests.test_oracle_vs_ref import _per_call_cases
-    for cr, fl, noise, depth, call, seed in _per_call_cases():
-        s = synth.viterbi_soft(cr, fl, noise, seed=seed)
-        Z.viterbi_brick_init_fast(fl, cr, depth)
-        d = oracle.Viterbi()
-        d.init(fl, cr, depth)
-        for k in range(0, s.size, call):
-            c = np.ascontiguousarray(s[k:k + call])
-            if c.size % 12:
-                break
-            nb, got = Z.viterbi_brick_decode_fast(c)
-            exp = d.decode(c)
-            assert nb == 8 * exp.size and (got == exp).all(), (cr, fl, depth, call, k)
-
-
-def test_viterbi_per_call_deep_windows_vs_oracle(oracle):
-    """Depths whose traceback window (depth + 24..31 lookahead columns) fits the per-call
-    kernel's 4096-column LDS window, straddles it, and exceeds it (walked in device memory)."""
-    from tests.golden import synth
-    for cr, depth, call in ((0, 4060, 480), (2, 4070, 96), (0, 5000, 480), (1, 8000, 4800)):
-        s = synth.viterbi_soft(cr, 2000, 3, seed=depth)
-        Z.viterbi_brick_init_fast(2000, cr, depth)
-        d = oracle.Viterbi()
-        d.init(2000, cr, depth)
-        total = 0
-        for k in range(0, s.size - call + 1, call):
-            c = np.ascontiguousarray(s[k:k + call])
-            nb, got = Z.viterbi_brick_decode_fast(c)
-            exp = d.decode(c)
-            assert nb == 8 * exp.size and (got == exp).all(), (cr, depth, call, k)
-            total += exp.size
-        assert total >= depth // 8, (cr, depth, total)
-
-
 def test_viterbi_batch_random_vs_oracle(oracle):
     rng = np.random.default_rng(77)
     softs, offs, fls, crs = [], [0], [], []
@@ -217,24 +118,6 @@ def test_viterbi_empty_batch():
     out, off = Z.viterbi_batch_decode(np.zeros(0, np.int8), np.array([0], np.int32),
                                       np.zeros(0, np.int32), np.zeros(0, np.int16))
     assert off.size == 0
-
-
-# ------------------------------------------------------------------ SIGNAL
-def test_signal_kat(golden):
-    k = golden["ref_kats"]
-    w = Z.viterbiSig11a_brick_decode_fast(k["sig_kat_soft"])
-    bits = np.unpackbits(w, bitorder="little")[:24].copy()
-    bits[18:] = 0
-    assert (bits == k["sig_kat_bits"]).all()
-
-
-def test_signal_reference_vectors(golden):
-    g = golden["ref_viterbi"]
-    for s, exp in zip(g["sig_soft"], g["sig_bits"]):
-        w = Z.viterbiSig11a_brick_decode_fast(s)
-        b = np.unpackbits(w, bitorder="little")[:24].copy()
-        b[18:] = 0
-        assert (np.packbits(b, bitorder="little") == exp).all()
 
 
 # ------------------------------------------------------------------ full chain

@@ -2,6 +2,9 @@
 
 The library is the product: ziria_amd's Python layer only loads it.  Output:
 ziria_amd/_lib/libziria_rx.so (git-ignored, travels to the GPU box with the snapshot).
+Translation units: zrx_api.hip (kernels, device API, batched externals; hipcc for gfx950),
+zrx_host.cpp (the per-call externals on the host CPU, AVX2) and zrx_ext_cxx.cpp (the
+externals with the C++ linkage wplc output links against), the last two with g++.
 """
 import os
 import subprocess
@@ -18,12 +21,15 @@ def source_hash():
     PMC summary in profiles/ to the kernels it was measured on (bench.py traffic fields)."""
     import hashlib
     h = hashlib.sha256()
-    files = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".hpp", ".h", ".py")))
+    files = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".hpp", ".h", ".py", ".cpp")))
     for f in files:
         h.update(f.encode())
         h.update(open(os.path.join(CSRC, f), "rb").read())
     h.update(open(os.path.join(HERE, "..", "include", "ziria_rx.h"), "rb").read())
     return h.hexdigest()[:16]
+
+
+HOST_SRCS = ("zrx_host.cpp", "zrx_ext_cxx.cpp")   # host-only TUs, g++
 
 
 def _stale():
@@ -68,8 +74,17 @@ def build(force=False, verbose=False):
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
     subprocess.check_call([sys.executable, os.path.join(CSRC, "gen_tables.py")])
+    objs = []
+    for src in HOST_SRCS:
+        obj = os.path.join(LIBDIR, os.path.splitext(src)[0] + ".o")
+        cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-mavx2", "-Wall", "-Wextra", "-c", "-o", obj,
+               os.path.join(CSRC, src)]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.check_call(cmd, cwd=CSRC)
+        objs.append(obj)
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-o", LIB + ".tmp", os.path.join(CSRC, "zrx_api.hip")]
+           "-Wall", "-o", LIB + ".tmp", os.path.join(CSRC, "zrx_api.hip"), "-x", "none"] + objs
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd, cwd=CSRC)

@@ -1,8 +1,10 @@
-// Host side of libziria_rx.so: the C-ABI of include/ziria_rx.h.
+// Host side of libziria_rx.so: the device API (Part 3) and the batched externals (Part 2) of
+// include/ziria_rx.h.
 //
-// Everything that computes runs in the HIP kernels of zrx_kernels.hip on a gfx950 device;
-// this file only validates arguments, stages buffers and launches.  Without a usable GPU
-// every entry point fails loudly (message on stderr + error code); there is no CPU path.
+// Everything here computes in the HIP kernels of zrx_kernels.hip on a gfx950 device; this
+// file only validates arguments, stages buffers and launches.  Without a usable GPU every
+// entry point fails loudly (message on stderr + error code); there is no CPU fallback.  The
+// per-call externals (Part 1) are the host path of zrx_host.cpp, by design.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -14,7 +16,9 @@
 #include <mutex>
 #include <vector>
 
+#define ZRX_C_LINKAGE_EXTERNALS
 #include "../../include/ziria_rx.h"
+#include "zrx_internal.h"
 #include "zrx_kernels.hip"
 
 using namespace zrx;
@@ -84,17 +88,12 @@ struct zrx_ctx {
   FftPlan* fft_plans = nullptr;
   uint32_t* fft_tw = nullptr;
   uint16_t* fft_pos = nullptr;
-  // per-call externals
-  VitStream* vstream = nullptr;
-  void* small = nullptr;          // staging for single calls
+  void* small = nullptr;          // staging of the batched externals' host arrays
   size_t small_cap = 0;
   hipStream_t side = nullptr;     // k_pkt_rows beside k_data_fft (rx chain, mixed batches)
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int32_t* mixed_hint = nullptr;  // pinned, mapped: 1 when the last planned batch was mixed
   int32_t* mixed_hint_dev = nullptr;
-  uint8_t* hsmall = nullptr;      // pinned, device-mapped staging the per-call kernels read and write in place
-  uint8_t* hsmall_dev = nullptr;
-  size_t hsmall_cap = 0;
 };
 
 static int check_device(int device) {
@@ -375,75 +374,13 @@ static void launch_viterbi(zrx_ctx* c, const uint8_t* soft, const int64_t* soft_
         soft, soft_off, params, npkts, out, out_off, out_bits, nullptr, c->nrows, c->segs, c->dumps);
 }
 
-// ---- FFTSafe<N> plans (zrx_fftn.hpp) ------------------------------------------------
-// The sizes of __ext_sora_fft (csrc/sora_ext_lib.cpp:2672-2812), the first-stage radix of
-// each (FFTSSEEx<N> specialisations: radix 3 csrc/sora_ext_lib_fft.hpp:190-251, radix 5
-// :366-430, radix 4 otherwise, base cases 4 / 8), and the frequency index each position holds
-// after the stages (a radix-4 stage leaves residues 0, 2, 1, 3 in its quarters, radix 3 / 5
-// in order, the base cases bit-reversed) — the same recursion as oracle/ziria_oracle.c.
-static const int kFftSizeList[kFftSizes] = {16, 32, 64, 128, 256, 512, 1024, 2048, 12, 24, 36, 48, 60, 72,
-                                            96, 108, 120, 144, 180, 192, 216, 240, 288, 300, 324, 360, 384,
-                                            432, 480, 540, 576, 600, 648, 720, 768, 864, 900, 960, 972, 1080,
-                                            1152, 1200};
-static int fftn_radix(int N) {
-  switch (N) {
-    case 4: case 8: return 0;
-    case 12: case 24: case 36: case 72: case 108: case 216: case 324: case 648: case 972: return 3;
-    case 60: case 120: case 180: case 300: case 360: case 540: case 600: case 900: case 1080: return 5;
-    default: return 4;
-  }
-}
-static void fftn_freq(int N, int* idx) {
-  const int r = fftn_radix(N);
-  if (r == 0) {
-    for (int p = 0; p < N; p++) idx[p] = N == 4 ? ((p & 1) << 1 | (p >> 1)) : ((p & 1) << 2 | (p & 2) | (p >> 2));
-    return;
-  }
-  const int M = N / r;
-  std::vector<int> sub(M);
-  fftn_freq(M, sub.data());
-  static const int res4[4] = {0, 2, 1, 3};
-  for (int q = 0; q < r; q++)
-    for (int p = 0; p < M; p++) idx[q * M + p] = r * sub[p] + (r == 4 ? res4[q] : q);
-}
-// twFFTLUT{M}_{k}[n] (csrc/sora_ext_lib_fft_coeffs.hpp): round(32768 e^{-j 2 pi k n / M}),
-// each part clamped to +-32767 (the oracle's zo_twiddle, checked against the brick)
-static uint32_t fftn_twiddle(int M, int k, int n) {
-  const double ang = -2.0 * M_PI * (double)k * (double)n / (double)M;
-  double r = std::floor(32768.0 * std::cos(ang) + 0.5), i = std::floor(32768.0 * std::sin(ang) + 0.5);
-  r = std::min(32767.0, std::max(-32767.0, r));
-  i = std::min(32767.0, std::max(-32767.0, i));
-  return (uint32_t)(uint16_t)(int16_t)r | ((uint32_t)(uint16_t)(int16_t)i << 16);
-}
-static int fftn_index(int N) {
-  for (int i = 0; i < kFftSizes; i++)
-    if (kFftSizeList[i] == N) return i;
-  return -1;
-}
+// ---- FFTSafe<N> plans (zrx_fftplan.hpp), uploaded once per context --------------------
 static int fftn_plans(zrx_ctx* c) {
   if (c->fft_plans) return ZRX_OK;
-  std::vector<FftPlan> plans(kFftSizes);
-  std::vector<uint32_t> tw;
-  std::vector<uint16_t> pos;
-  for (int i = 0; i < kFftSizes; i++) {
-    const int N = kFftSizeList[i];
-    FftPlan& P = plans[i];
-    P.N = N; P.nst = 0;
-    for (int M = N;;) {
-      const int r = fftn_radix(M);
-      FftStage& st = P.st[P.nst++];
-      st.radix = (uint16_t)r; st.M = (uint16_t)M; st.tw = (uint32_t)tw.size();
-      if (r == 0) break;
-      for (int k = 1; k < r; k++)
-        for (int n = 0; n < M / r; n++) tw.push_back(fftn_twiddle(M, k, n));
-      M /= r;
-    }
-    std::vector<int> idx(N);
-    fftn_freq(N, idx.data());
-    P.pos = (uint32_t)pos.size();
-    pos.resize(pos.size() + N);
-    for (int p = 0; p < N; p++) pos[P.pos + idx[p]] = (uint16_t)p;
-  }
+  const FftPlans R = fftn_build_plans();
+  const std::vector<FftPlan>& plans = R.plans;
+  const std::vector<uint32_t>& tw = R.tw;
+  const std::vector<uint16_t>& pos = R.pos;
   ZRX_CHECK(hipSetDevice(c->device));
   ZRX_CHECK(hipMalloc(&c->fft_plans, sizeof(FftPlan) * kFftSizes));
   ZRX_CHECK(hipMalloc(&c->fft_tw, tw.size() * 4));
@@ -510,10 +447,8 @@ int zrx_destroy(zrx_ctx* c) {
   for (void* p : {(void*)c->fe_pattern, (void*)c->fe_syms, (void*)c->fe_sym_off, (void*)c->fe_nsym, (void*)c->fe_chan,
                   (void*)c->tx_preamble})
     (void)hipFree(p);
-  (void)hipFree(c->vstream);
   for (void* p : {(void*)c->fft_plans, (void*)c->fft_tw, (void*)c->fft_pos}) (void)hipFree(p);
   (void)hipFree(c->small);
-  if (c->hsmall) (void)hipHostFree(c->hsmall);
   if (c->mixed_hint) (void)hipHostFree(c->mixed_hint);
   for (auto& set : c->evsets)
     for (auto& e : set) (void)hipEventDestroy(e);
@@ -852,18 +787,19 @@ int zrx_trig_tables(int16_t* sin65536, int16_t* cos65536, int16_t* atan65536) {
 
 }  // extern "C"
 
-// ------------------------------------------------------------------ default context (per-call API)
+// ------------------------------------------------------------------ batched externals (host arrays)
+// The per-call externals (Part 1 of ziria_rx.h) run on the host: zrx_host.cpp.  The batched
+// ones below stage host arrays through one default GPU context and launch the chain.
 static std::mutex g_mu;
 static zrx_ctx* g_ctx = nullptr;
 
+// The default context (device of the calling thread), created on first use; nullptr without
+// a gfx950 device: the batched externals then return ZRX_ENODEV (they have no CPU path).
 static zrx_ctx* default_ctx() {
   if (g_ctx) return g_ctx;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-  if (zrx_create(&g_ctx, dev, nullptr) != ZRX_OK) {
-    std::fprintf(stderr, "ziria_rx: cannot create a GPU context; the externals have no CPU path\n");
-    std::abort();   // the reference would be unusable too; fail loudly rather than compute wrongly
-  }
+  if (zrx_create(&g_ctx, dev, nullptr) != ZRX_OK) g_ctx = nullptr;
   return g_ctx;
 }
 
@@ -879,28 +815,12 @@ static void* staging(zrx_ctx* c, size_t bytes) {
 }
 
 // Pinned host memory mapped into the device's address space (coherent: the GPU does not
-// cache it), so a per-call external's kernel reads its input and writes its output in place:
-// one launch and one stream sync per call, no DMA copies (each costs ~10 us at this size).
+// cache it); the rx chain's mixed-batch hint word lives there.
 static void* pinned_mapped(size_t bytes, void** dev) {
   void* h = nullptr;
   if (hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
   if (hipHostGetDevicePointer(dev, h, 0) != hipSuccess) { (void)hipHostFree(h); return nullptr; }
   return h;
-}
-static uint8_t* hstaging(zrx_ctx* c, size_t bytes, uint8_t** dev) {
-  if (bytes > c->hsmall_cap) {
-    if (c->hsmall) (void)hipHostFree(c->hsmall);
-    c->hsmall = nullptr;
-    c->hsmall_cap = 0;
-    const size_t cap = std::max<size_t>(bytes, 1 << 16);
-    void* dp = nullptr;
-    c->hsmall = (uint8_t*)pinned_mapped(cap, &dp);
-    if (!c->hsmall) return nullptr;
-    c->hsmall_dev = (uint8_t*)dp;
-    c->hsmall_cap = cap;
-  }
-  *dev = c->hsmall_dev;
-  return c->hsmall;
 }
 
 #define ZRX_DIE(msg)                                                     \
@@ -911,168 +831,17 @@ static uint8_t* hstaging(zrx_ctx* c, size_t bytes, uint8_t** dev) {
 #define ZRX_OR_DIE(call) \
   do { if ((call) != hipSuccess) ZRX_DIE(#call); } while (0)
 
-extern "C" {
+namespace zrx_batch {
 
-// csrc/sora_ext_lib.cpp:2672-2812: every size the reference dispatches; any other prints the
-// reference's message and leaves the output untouched (:2808-2810).
-void __ext_sora_fft(struct complex16* out, int nFFTSize, struct complex16* in, int unused1) {
-  (void)unused1;
-  if (fftn_index(nFFTSize) < 0) {
-    std::printf("__ext_sora_fft error: fft size %d not supported!\n", nFFTSize);
-    return;
-  }
-  std::lock_guard<std::mutex> lk(g_mu);
-  zrx_ctx* c = default_ctx();
-  ZRX_OR_DIE(fftn_plans(c) == ZRX_OK ? hipSuccess : hipErrorUnknown);
-  const size_t bytes = (size_t)nFFTSize * 4;
-  uint8_t* d = nullptr;
-  uint8_t* h = hstaging(c, 2 * bytes, &d);
-  if (!h) ZRX_DIE("pinned staging allocation failed");
-  std::memcpy(h, in, bytes);
-  launch_fft(c, nFFTSize, d, d + bytes, 1);
-  ZRX_OR_DIE(hipGetLastError());
-  ZRX_OR_DIE(hipStreamSynchronize(c->stream));
-  std::memcpy(out, h + bytes, bytes);
-}
-
-void __ext_sora_fft_dynamic(struct complex16* out, int unused2, int16_t nFFTSize, struct complex16* in, int unused1) {
-  (void)unused2;
-  __ext_sora_fft(out, nFFTSize, in, unused1);
-}
-
-// The streaming decoder behind the per-call externals.  Its trellis state lives on the GPU
-// (VitStream); the host mirrors only the brick's schedule (trellis index and bits output,
-// sora_ext_viterbi.cpp:112-149), which depends on nothing but the group count.  A call whose
-// groups reach no traceback returns 0 bits in the reference, so its soft values are only
-// queued in pinned host memory; the call that reaches a traceback runs every queued group
-// and its own in one launch and copies back exactly the bytes the schedule says it emits.
-struct VitHost {
-  bool ready = false;
-  uint32_t tr = 0, ob = 0, tr_end = 0, depth = 256;
-  int cr = 0;
-  uint8_t* pend = nullptr;         // queued soft values (pinned, mapped: the kernel reads them in place)
-  uint8_t* pend_dev = nullptr;
-  size_t npend = 0, cap = 0;
-  uint8_t* out = nullptr;          // pinned, mapped: the kernel writes the call's bytes here, bit count at the end
-  uint8_t* out_dev = nullptr;
-  size_t out_cap = 0;
-};
-static VitHost g_vh;
-
-static int vit_init_impl(int32_t frame_len, int16_t code_rate, int16_t depth) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  zrx_ctx* c = default_ctx();
-  if (!c->vstream) ZRX_OR_DIE(hipMalloc(&c->vstream, sizeof(VitStream)));
-  k_vit_init<<<1, 64, 0, c->stream>>>(c->vstream, frame_len, code_rate, depth);
-  ZRX_OR_DIE(hipGetLastError());
-  g_vh.ready = true;
-  g_vh.tr = 0; g_vh.ob = 0;
-  g_vh.tr_end = (uint32_t)frame_len * 8u + 6u;
-  g_vh.depth = (uint32_t)depth;
-  g_vh.cr = code_rate;
-  g_vh.npend = 0;                                    // groups of the previous frame: no output left
-  return 0;
-}
-
-int __ext_viterbi_brick_init_fast(int32_t frame_len, int16_t code_rate, int16_t depth) {
-  return vit_init_impl(frame_len, code_rate, depth);
-}
-int __ext_viterbiSig11a_brick_init_fast(int32_t frame_len, int16_t code_rate, int16_t depth) {
-  return vit_init_impl(frame_len, code_rate, depth);    // the reference resets the same decoder
-}
-
-int16_t __ext_viterbi_brick_decode_fast(int8_t* intInput, int len1, unsigned char* bit, int len2) {
-  (void)len2;
-  if (len1 <= 0) return 0;
-  std::lock_guard<std::mutex> lk(g_mu);
-  zrx_ctx* c = default_ctx();
-  if (!c->vstream || !g_vh.ready) ZRX_DIE("__ext_viterbi_brick_decode_fast before __ext_viterbi_brick_init_fast");
-  VitHost& h = g_vh;
-  const int G = h.cr == 0 ? 2 : h.cr == 1 ? 3 : h.cr == 2 ? 4 : 0;
-  const uint32_t steps = h.cr == 0 ? 1u : h.cr == 1 ? 2u : 3u;
-  if (G == 0) return 0;
-  const size_t n = (size_t)(len1 / G) * G;          // whole groups (k_viterbi_stream drops a partial one)
-  uint32_t bytes = 0;                                // what this call emits (:112-149)
-  for (size_t k = 0; k < n; k += G) {
-    h.tr += steps;
-    uint32_t cnt = 0;
-    if (h.tr >= h.tr_end) cnt = h.tr_end - h.ob - 6u;
-    else if (h.tr >= h.ob + h.depth + 30u) cnt = h.depth;
-    if (cnt) { bytes += cnt >> 3; h.ob += cnt; }
-  }
-  if (h.npend + n + 64 > h.cap) {                    // +64: the kernel reads whole dwords past the end
-    const size_t cap = std::max<size_t>(h.npend + n + 64, std::max<size_t>(2 * h.cap, 1 << 16));
-    void* dp = nullptr;
-    uint8_t* np = (uint8_t*)pinned_mapped(cap, &dp);
-    if (!np) ZRX_DIE("pinned allocation failed");
-    if (h.npend) std::memcpy(np, h.pend, h.npend);
-    if (h.pend) (void)hipHostFree(h.pend);
-    h.pend = np; h.pend_dev = (uint8_t*)dp; h.cap = cap;
-  }
-  std::memcpy(h.pend + h.npend, intInput, n);
-  h.npend += n;
-  if (bytes == 0) return 0;                          // no traceback in this call: stays queued
-  if (bytes + 16 > h.out_cap) {
-    if (h.out) (void)hipHostFree(h.out);
-    h.out_cap = std::max<size_t>(((bytes + 15) / 16) * 16 + 16, 4096);
-    void* dp = nullptr;
-    h.out = (uint8_t*)pinned_mapped(h.out_cap, &dp);
-    if (!h.out) ZRX_DIE("pinned allocation failed");
-    h.out_dev = (uint8_t*)dp;
-  }
-  k_viterbi_stream<<<1, 64, 0, c->stream>>>(c->vstream, h.pend_dev, (int)h.npend, h.out_dev,
-                                            (int32_t*)(h.out_dev + h.out_cap - 16));
-  ZRX_OR_DIE(hipGetLastError());
-  ZRX_OR_DIE(hipStreamSynchronize(c->stream));
-  std::memcpy(bit, h.out, bytes);
-  h.npend = 0;
-  return (int16_t)(bytes * 8u);
-}
-
-int16_t __ext_viterbiSig11a_brick_decode_fast(int8_t* intInput, int len1, unsigned char* bit, int len2) {
-  (void)len1; (void)len2;
-  std::lock_guard<std::mutex> lk(g_mu);
-  zrx_ctx* c = default_ctx();
-  uint8_t* d = nullptr;
-  uint8_t* h = hstaging(c, 128, &d);
-  if (!h) ZRX_DIE("pinned staging allocation failed");
-  std::memcpy(h, intInput, 48);
-  k_sig_bytes<<<1, 64, 0, c->stream>>>((const uint32_t*)d, 1, d + 64);
-  ZRX_OR_DIE(hipGetLastError());
-  ZRX_OR_DIE(hipStreamSynchronize(c->stream));
-  std::memcpy(bit, h + 64, 3);
-  uint32_t w;
-  std::memcpy(&w, bit, 4);
-  w >>= 6;                                            // *((unum32 *)bit) >>= 6  (:191)
-  std::memcpy(bit, &w, 4);
-  return 0;
-}
-
-int __ext_v_shift_right_complex16(struct complex16* z, int unused3, struct complex16* x, int len, int shift) {
-  (void)unused3;
-  if (len <= 0) return 0;
-  std::lock_guard<std::mutex> lk(g_mu);
-  zrx_ctx* c = default_ctx();
-  const size_t bytes = (size_t)len * 4;
-  uint8_t* d = (uint8_t*)staging(c, 2 * bytes + 64);
-  if (!d) ZRX_DIE("staging allocation failed");
-  uint8_t* dz = d + ((bytes + 15) / 16) * 16;
-  ZRX_OR_DIE(hipMemcpyAsync(d, x, bytes, hipMemcpyHostToDevice, c->stream));
-  k_shift_right<<<blocks(2 * (int64_t)len, 256), 256, 0, c->stream>>>((const uint16_t*)d, (uint16_t*)dz, len, shift);
-  ZRX_OR_DIE(hipGetLastError());
-  ZRX_OR_DIE(hipMemcpyAsync(z, dz, bytes, hipMemcpyDeviceToHost, c->stream));
-  ZRX_OR_DIE(hipStreamSynchronize(c->stream));
-  return 0;
-}
-
-// ------------------------------------------------------------------ batched, host arrays
-void __ext_sora_fft64_batch(struct complex16* out, int outlen, struct complex16* in, int inlen) {
+// nsym independent FFT64s (no return value to carry an error: fails loudly without a GPU)
+void sora_fft64_batch(struct complex16* out, int outlen, struct complex16* in, int inlen) {
   if (inlen <= 0 || inlen % 64 || outlen < inlen) {
     std::fprintf(stderr, "ziria_rx: __ext_sora_fft64_batch needs inlen = 64*k and outlen >= inlen\n");
     return;
   }
   std::lock_guard<std::mutex> lk(g_mu);
   zrx_ctx* c = default_ctx();
+  if (!c) ZRX_DIE("no gfx950 device: the batched externals run on the GPU");
   const size_t bytes = (size_t)inlen * 4;
   uint8_t* d = (uint8_t*)staging(c, 2 * bytes);
   if (!d) ZRX_DIE("staging allocation failed");
@@ -1082,9 +851,10 @@ void __ext_sora_fft64_batch(struct complex16* out, int outlen, struct complex16*
   ZRX_OR_DIE(hipStreamSynchronize(c->stream));
 }
 
-int32_t __ext_viterbi_batch_decode(int8_t* soft, int softlen, int32_t* pkt_soft_off, int n_off,
-                                   int32_t* frame_len, int n_fl, int16_t* code_rate, int n_cr,
-                                   unsigned char* out_bits, int out_len_bits, int32_t* pkt_out_off, int n_oo) {
+
+int32_t viterbi_batch_decode(const char* soft, int softlen, const int32_t* pkt_soft_off, int n_off,
+                             const int32_t* frame_len, int n_fl, const int16_t* code_rate, int n_cr,
+                             unsigned char* out_bits, int out_len_bits, const int32_t* pkt_out_off, int n_oo) {
   const int np = n_off - 1;
   if (np < 0 || n_fl < np || n_cr < np || n_oo < np || softlen < 0 || out_len_bits < 0) return ZRX_EINVAL;
   if (np == 0) return 0;
@@ -1103,6 +873,7 @@ int32_t __ext_viterbi_batch_decode(int8_t* soft, int softlen, int32_t* pkt_soft_
   }
   std::lock_guard<std::mutex> lk(g_mu);
   zrx_ctx* c = default_ctx();
+  if (!c) return ZRX_ENODEV;
   int rc0 = zrx_reserve(c, np, 1);                   // room for the row plan of k_pkt_plan
   if (rc0) return rc0;
   const size_t s_soft = ((size_t)softlen + 255) / 256 * 256, s_par = (size_t)np * 16, s_off = (size_t)np * 8;
@@ -1127,12 +898,16 @@ int32_t __ext_viterbi_batch_decode(int8_t* soft, int softlen, int32_t* pkt_soft_
   return np;
 }
 
-static int32_t wifi_rx_batch_impl(struct complex16* sym, int nsym_total, int32_t* pkt_sym_off, int n_off,
-                                  const struct complex16* chan, unsigned char* payload, int payload_len_bits,
-                                  int32_t* pkt_info, int n_info) {
+
+// receiveBits over host packets; chan (64 coefficients per packet, chan_len >= 64 npkts) adds
+// ChannelEqualization + PilotTrack
+int32_t wifi_rx_batch(struct complex16* sym, int nsym_total, const int32_t* pkt_sym_off, int n_off,
+                      const struct complex16* chan, int chan_len, unsigned char* payload, int payload_len_bits,
+                      int32_t* pkt_info, int n_info) {
   const int np = n_off - 1;
   if (np < 0 || nsym_total < 0 || n_info < 8 * np || (int64_t)payload_len_bits / 8 < (int64_t)np * kPayloadStride)
     return ZRX_EINVAL;
+  if (chan && chan_len < 64 * (int64_t)np) return ZRX_EINVAL;
   if (np == 0) return 0;
   std::vector<int64_t> off(np);
   std::vector<int32_t> ns(np);
@@ -1145,6 +920,7 @@ static int32_t wifi_rx_batch_impl(struct complex16* sym, int nsym_total, int32_t
   }
   std::lock_guard<std::mutex> lk(g_mu);
   zrx_ctx* c = default_ctx();
+  if (!c) return ZRX_ENODEV;
   int rc = zrx_reserve(c, np, max_ns);
   if (rc) return rc;
   const size_t s_sym = ((size_t)nsym_total * 256 + 255) / 256 * 256 + 256;
@@ -1174,22 +950,10 @@ static int32_t wifi_rx_batch_impl(struct complex16* sym, int nsym_total, int32_t
   return ok;
 }
 
-int32_t __ext_wifi_rx_batch(struct complex16* sym, int nsym_total, int32_t* pkt_sym_off, int n_off,
-                            unsigned char* payload, int payload_len_bits, int32_t* pkt_info, int n_info) {
-  return wifi_rx_batch_impl(sym, nsym_total, pkt_sym_off, n_off, nullptr, payload, payload_len_bits, pkt_info, n_info);
-}
 
-int32_t __ext_wifi_rx_eq_batch(struct complex16* sym, int nsym_total, int32_t* pkt_sym_off, int n_off,
-                               struct complex16* chan, int chan_len, unsigned char* payload, int payload_len_bits,
-                               int32_t* pkt_info, int n_info) {
-  const int np = n_off - 1;
-  if (np < 0 || !chan || chan_len < 64 * np) return ZRX_EINVAL;
-  return wifi_rx_batch_impl(sym, nsym_total, pkt_sym_off, n_off, chan, payload, payload_len_bits, pkt_info, n_info);
-}
-
-int32_t __ext_wifi_rx_stream_batch(struct complex16* samples, int nsamples, int32_t* cap_off, int n_off,
-                                   int downsample, unsigned char* payload, int payload_len_bits,
-                                   int32_t* pkt_info, int n_info, int32_t* det, int n_det) {
+int32_t wifi_rx_stream_batch(struct complex16* samples, int nsamples, const int32_t* cap_off, int n_off,
+                             int downsample, unsigned char* payload, int payload_len_bits,
+                             int32_t* pkt_info, int n_info, int32_t* det, int n_det) {
   const int nc = n_off - 1;
   if (nc < 0 || nsamples < 0 || n_info < 8 * nc || n_det < fe::kDetWords * nc ||
       (int64_t)payload_len_bits / 8 < (int64_t)nc * kPayloadStride)
@@ -1206,6 +970,7 @@ int32_t __ext_wifi_rx_stream_batch(struct complex16* samples, int nsamples, int3
   }
   std::lock_guard<std::mutex> lk(g_mu);
   zrx_ctx* c = default_ctx();
+  if (!c) return ZRX_ENODEV;
   const size_t s_smp = ((size_t)nsamples * 4 + 255) / 256 * 256 + 256;
   const size_t s_off = ((size_t)nc * 8 + 255) / 256 * 256, s_len = ((size_t)nc * 4 + 255) / 256 * 256;
   const size_t s_pay = (size_t)nc * kPayloadStride, s_info = ((size_t)nc * 32 + 255) / 256 * 256;
@@ -1233,8 +998,9 @@ int32_t __ext_wifi_rx_stream_batch(struct complex16* samples, int nsamples, int3
   return ok;
 }
 
-int32_t __ext_wifi_tx_batch(unsigned char* in, int inlen, int32_t* pkt_in_off, int n_off,
-                            struct complex16* out, int outlen, int32_t* pkt_out_off, int n_oo) {
+
+int32_t wifi_tx_batch(const unsigned char* in, int inlen, const int32_t* pkt_in_off, int n_off,
+                      struct complex16* out, int outlen, int32_t* pkt_out_off, int n_oo) {
   const int np = n_off - 1;
   if (np < 0 || inlen < 0 || n_oo < np + 1) return ZRX_EINVAL;
   if (np == 0) { pkt_out_off[0] = 0; return 0; }
@@ -1254,6 +1020,7 @@ int32_t __ext_wifi_tx_batch(unsigned char* in, int inlen, int32_t* pkt_in_off, i
   if (total > outlen) return ZRX_EINVAL;
   std::lock_guard<std::mutex> lk(g_mu);
   zrx_ctx* c = default_ctx();
+  if (!c) return ZRX_ENODEV;
   const size_t s_in = ((size_t)inlen + 255) / 256 * 256 + 256, s_off = ((size_t)np * 8 + 255) / 256 * 256;
   const size_t s_out = (size_t)total * 4;
   uint8_t* d = (uint8_t*)staging(c, s_in + 2 * s_off + s_off / 2 + s_out + 1024);
@@ -1271,6 +1038,44 @@ int32_t __ext_wifi_tx_batch(unsigned char* in, int inlen, int32_t* pkt_in_off, i
   ZRX_CHECK(hipMemcpyAsync(out, d_out, s_out, hipMemcpyDeviceToHost, c->stream));
   ZRX_CHECK(hipStreamSynchronize(c->stream));
   return (int32_t)total;
+}
+
+
+}  // namespace zrx_batch
+
+// C linkage (ctypes, C callers); zrx_ext_cxx.cpp exports the same with C++ linkage
+extern "C" {
+
+void __ext_sora_fft64_batch(struct complex16* out, int outlen, struct complex16* in, int inlen) {
+  zrx_batch::sora_fft64_batch(out, outlen, in, inlen);
+}
+int32_t __ext_viterbi_batch_decode(char* soft, int softlen, int32_t* pkt_soft_off, int n_off,
+                                   int32_t* frame_len, int n_fl, int16_t* code_rate, int n_cr,
+                                   unsigned char* out_bits, int out_len_bits, int32_t* pkt_out_off, int n_oo) {
+  return zrx_batch::viterbi_batch_decode(soft, softlen, pkt_soft_off, n_off, frame_len, n_fl, code_rate, n_cr,
+                                         out_bits, out_len_bits, pkt_out_off, n_oo);
+}
+int32_t __ext_wifi_rx_batch(struct complex16* sym, int nsym_total, int32_t* pkt_sym_off, int n_off,
+                            unsigned char* payload, int payload_len_bits, int32_t* pkt_info, int n_info) {
+  return zrx_batch::wifi_rx_batch(sym, nsym_total, pkt_sym_off, n_off, nullptr, 0, payload, payload_len_bits,
+                                  pkt_info, n_info);
+}
+int32_t __ext_wifi_rx_eq_batch(struct complex16* sym, int nsym_total, int32_t* pkt_sym_off, int n_off,
+                               struct complex16* chan, int chan_len, unsigned char* payload, int payload_len_bits,
+                               int32_t* pkt_info, int n_info) {
+  if (!chan) return ZRX_EINVAL;
+  return zrx_batch::wifi_rx_batch(sym, nsym_total, pkt_sym_off, n_off, chan, chan_len, payload, payload_len_bits,
+                                  pkt_info, n_info);
+}
+int32_t __ext_wifi_rx_stream_batch(struct complex16* samples, int nsamples, int32_t* cap_off, int n_off,
+                                   int downsample, unsigned char* payload, int payload_len_bits,
+                                   int32_t* pkt_info, int n_info, int32_t* det, int n_det) {
+  return zrx_batch::wifi_rx_stream_batch(samples, nsamples, cap_off, n_off, downsample, payload, payload_len_bits,
+                                         pkt_info, n_info, det, n_det);
+}
+int32_t __ext_wifi_tx_batch(unsigned char* in, int inlen, int32_t* pkt_in_off, int n_off,
+                            struct complex16* out, int outlen, int32_t* pkt_out_off, int n_oo) {
+  return zrx_batch::wifi_tx_batch(in, inlen, pkt_in_off, n_off, out, outlen, pkt_out_off, n_oo);
 }
 
 }  // extern "C"

@@ -1,36 +1,15 @@
 // FFTSafe<N> for every size __ext_sora_fft dispatches (csrc/sora_ext_lib.cpp:2672-2812):
 // 16..2048 and the LTE sizes 12..1200, one workgroup per transform, the N values in LDS.
 //
-// The reference recursion (FFTSSEEx<N>, csrc/fft_r4difx.hpp:99-218; FFTSSE_3W / FFTSSE_5W,
-// csrc/sora_ext_lib_fft.hpp:111-430) applies one DIF stage to the whole block and recurses
-// into its r sub-blocks; every sub-block at one depth has the same size, so the transform
-// is a list of stages (radix r on sub-blocks of M), each a set of independent butterflies
-// that the workgroup's threads share between two barriers.  Per butterfly the integer
-// semantics are the SSE bricks' (saturating int16 adds, madd-wrap mul_shift, XOR-as-
-// negate), so the result is bit-exact; the output permutation (the reference's
-// bFFT{N}LUTMap) comes from the same recursion (oracle/ziria_oracle.c zo_fft_freq_of_pos).
-// The host (zrx_api.hip fftn_plans) builds one FftPlan per size with its twiddles
-// (round(32768 e^{-j2pi k n / M}) clamped to +-32767, the reference tables' formula) and
-// the position of every output bin.
+// The plans (stage list, twiddles, output positions) come from zrx_fftplan.hpp; each stage's
+// butterflies are independent, so the workgroup's threads share them between two barriers.
+// Per butterfly the integer semantics are the SSE bricks' (saturating int16 adds, madd-wrap
+// mul_shift, XOR-as-negate), so the result is bit-exact.
 #pragma once
 #include "zrx_device.hpp"
+#include "zrx_fftplan.hpp"
 
 namespace zrx {
-
-constexpr int kFftMaxN = 2048;
-constexpr int kFftMaxStages = 8;
-constexpr int kFftSizes = 42;
-
-struct FftStage {
-  uint16_t radix;       // 3, 4, 5: a DIF stage; 0: the base case (4 or 8 points, M = 4 / 8)
-  uint16_t M;           // sub-block size
-  uint32_t tw;          // twiddle offset: entry (k - 1) * (M / radix) + n = tw<M, k>[n]
-};
-struct FftPlan {
-  int32_t N, nst;
-  FftStage st[kFftMaxStages];
-  uint32_t pos;         // offset of N uint16: out[f] = x[pos[f]]
-};
 
 // FFTSSEEx<8> (csrc/fft_r4difx.hpp:142-218) per complex value: input >> 3; d = x[k] -
 // x[k+4], s = x[k] + x[k+4]; the lower half rotates d2, d3 by (im, ~re), pairs them with d0,

@@ -13,7 +13,6 @@
 //   k_viterbi        (experiment builds only) one wave per packet, lane = trellis state
 //   k_descramble_crc one wave per packet: descrambler (Decode.blk:36-43) + CRC-32 check
 //                    (crc.blk:85-118), 64 lanes each on a chunk, CRC combined by GF(2) maps
-//   k_viterbi_stream / k_vit_init / k_sig_bytes / k_shift_right: the per-call externals.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -545,7 +544,8 @@ __global__ __launch_bounds__(256) void k_ofdm_eq(const uint4* __restrict__ sym, 
   }
 }
 
-// ------------------------------------------------------------------ Viterbi brick, batched
+#ifdef ZRX_EXPERIMENTS   // the v1 batched kernel (lane = state): A/B builds only
+// ------------------------------------------------------------------ Viterbi brick, batched (v1)
 // Decoder state of the brick driver loop (sora_ext_viterbi.cpp:66-153) for one packet.
 struct VitRun {
   uint32_t m, tr, ob, total_bytes, tr_end, depth;
@@ -573,7 +573,6 @@ __device__ __forceinline__ void vit_after_group(VitRun& v, int lane, Surv surv, 
   }
 }
 
-#ifdef ZRX_EXPERIMENTS   // the v1 batched kernel (lane = state): A/B builds only
 template <int USE>
 __device__ __forceinline__ void vit_step(VitRun& v, int a, int b, const VitLane& L, int lane, uint64_t* ring) {
   v.m = acs<USE>(v.m, a, b, L);
@@ -769,139 +768,6 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
       in[4] = crc == rx ? 1 : 0;
     }
   }
-}
-
-// ------------------------------------------------------------------ per-call externals
-// Streaming decoder with the reference's global-brick semantics (sora_ext_viterbi.cpp:39-46):
-// full trellis history (TRELLIS_MAX = 40000 columns) in device memory.
-constexpr int kTrellisMax = 40000;
-struct VitStream {
-  uint32_t m[64];
-  uint32_t tr, ob, frame_len, code_rate, depth, pad[3];
-  uint64_t surv[kTrellisMax + 16];
-};
-__global__ void k_vit_init(VitStream* st, int frame_len, int code_rate, int depth) {
-  const int lane = threadIdx.x;
-  st->m[lane] = lane == 0 ? 0u : 48u;
-  if (lane == 0) {
-    st->tr = 0; st->ob = 0; st->frame_len = (uint32_t)frame_len; st->code_rate = (uint32_t)code_rate;
-    st->depth = (uint32_t)depth; st->surv[0] = 0;
-  }
-}
-struct SurvGlobal {
-  const uint64_t* s;
-  __device__ __forceinline__ uint64_t operator()(uint32_t t) const {
-    return __hip_atomic_load(s + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-};
-template <int USE>
-__device__ __forceinline__ void stream_step(VitRun& v, int a, int b, const VitLane& L, int lane, VitStream* st) {
-  v.m = acs<USE>(v.m, a, b, L);
-  v.tr++;
-  const uint64_t w = __ballot((v.m & 1u) != 0);
-  if (lane == 0 && v.tr < (uint32_t)(kTrellisMax + 16))
-    __hip_atomic_store(st->surv + v.tr, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// Survivor words of columns lo .. lo + n - 1 staged in LDS for one traceback.
-struct SurvWin {
-  const uint64_t* w;
-  uint32_t lo;
-  __device__ __forceinline__ uint64_t operator()(uint32_t t) const { return w[t - lo]; }
-};
-constexpr uint32_t kStreamWin = 4096;   // LDS window (32 KB): depth + lookahead up to 4096 columns
-
-// Normalize and traceback schedule as vit_after_group; the traceback window (its cnt + look
-// columns, written to device memory by lane 0 in this or an earlier call) is first copied
-// into LDS by the whole wave, so the walk's dependent reads are LDS reads, not L2 round trips.
-// A window beyond kStreamWin (depth > ~4060) walks device memory.
-__device__ __forceinline__ void stream_after_group(VitRun& v, int lane, const VitStream* st, uint64_t* win,
-                                                   uint8_t* __restrict__ out) {
-  if ((v.tr & 7u) == 0) v.m = vit_normalize(v.m);
-  uint32_t cnt = 0, look = 0;
-  if (v.tr >= v.tr_end) {
-    cnt = v.tr_end - v.ob - 6u;
-    look = v.tr - v.tr_end;
-  } else if (v.tr >= v.ob + v.depth + 30u) {
-    cnt = v.depth;
-    look = 24u + (v.tr - (v.ob + v.depth + 30u)) % 8u;
-  }
-  if (!cnt) return;
-  const uint32_t n = cnt + look, lo = v.tr - n;      // columns the walk reads: lo .. tr - 1
-  __builtin_amdgcn_s_waitcnt(0);                     // this wave's survivor stores have completed
-  if (n <= kStreamWin) {
-    for (uint32_t j = (uint32_t)lane; j < n; j += 64)
-      win[j] = __hip_atomic_load(st->surv + lo + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    vit_traceback(v.m, v.tr, cnt, look, lane, SurvWin{win, lo}, out + v.total_bytes);
-    __syncthreads();                                   // the window is rewritten by the next traceback
-  } else {
-    vit_traceback(v.m, v.tr, cnt, look, lane, SurvGlobal{st->surv}, out + v.total_bytes);
-  }
-  v.ob += cnt;
-  v.total_bytes += cnt >> 3;
-}
-
-// One decode call on n soft values (one wave).  out gets this call's bytes; *out_bits its bits.
-// Soft values are read 192 at a time (48 dwords, one per lane; 192 is a multiple of every
-// group size) and taken out with readlane, so no group waits on a memory load; the bytes and
-// the bit count go straight to the caller's pinned buffer.
-__global__ __launch_bounds__(64) void k_viterbi_stream(VitStream* st, const uint8_t* __restrict__ sp, int n,
-                                                       uint8_t* __restrict__ out, int32_t* __restrict__ out_bits) {
-  __shared__ uint64_t win[kStreamWin];
-  const int lane = threadIdx.x;
-  const VitLane L = vit_lane(lane);
-  VitRun v;
-  v.m = st->m[lane];
-  v.tr = st->tr; v.ob = st->ob; v.total_bytes = 0;
-  v.tr_end = st->frame_len * 8u + 6u; v.depth = st->depth; v.done = false;
-  const int cr = (int)st->code_rate;
-  const int G = cr == 0 ? 2 : (cr == 1 ? 3 : (cr == 2 ? 4 : 0));
-  // sp is pinned host memory (the host keeps it 16-B aligned with 64 B of slack): the next
-  // chunk's load is issued before this chunk's groups, so its latency hides behind them.
-  auto load = [sp, n, lane](int base) {
-    return (lane < 48 && base + 4 * lane < n) ? (int)((const uint32_t*)(sp + base))[lane] : 0;
-  };
-  if (G) {
-    int next = load(0);
-    for (int base = 0; base + G <= n; base += 192) {
-      const int chunk = next;
-      next = load(base + 192);
-      const int cn = min(192, n - base);
-      auto soft = [chunk](int q) { return (int)(((uint32_t)__builtin_amdgcn_readlane(chunk, q >> 2) >> (8 * (q & 3))) & 0xFFu); };
-      for (int k = 0; k + G <= cn; k += G) {
-        stream_step<3>(v, soft(k), soft(k + 1), L, lane, st);
-        if (cr == 2) { stream_step<1>(v, soft(k + 2), 0, L, lane, st); stream_step<2>(v, soft(k + 3), 0, L, lane, st); }
-        if (cr == 1) { stream_step<1>(v, soft(k + 2), 0, L, lane, st); }
-        stream_after_group(v, lane, st, win, out);   // the brick keeps running after the final traceback (0 bits)
-      }
-    }
-  }
-  st->m[lane] = v.m;
-  if (lane == 0) { st->tr = v.tr; st->ob = v.ob; *out_bits = (int32_t)(v.total_bytes * 8u); }
-}
-// Viterbi_sig11 for a batch: 3 traceback bytes per packet (before the brick's >>6).
-__global__ __launch_bounds__(256) void k_sig_bytes(const uint32_t* __restrict__ sig_soft, int npkts, uint8_t* __restrict__ out3) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int p = blockIdx.x * 4 + wv;
-  if (p >= npkts) return;
-  const uint32_t dw = lane < 12 ? sig_soft[(int64_t)p * 12 + lane] : 0u;
-  const uint32_t word = sig11_word(dw, lane);
-  if (lane < 3) out3[(int64_t)p * 3 + lane] = (uint8_t)(word >> (8 * lane));
-}
-// __ext_v_shift_right_complex16 (sora_ext_lib.cpp:1979-1995): the first len/4*4 complex
-// values use srai_epi16 (arithmetic); the tail uses unum16 >> shift (logical).
-__global__ void k_shift_right(const uint16_t* __restrict__ x, uint16_t* __restrict__ z, int len, int shift) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= 2 * len) return;
-  const uint16_t v = x[e];
-  uint16_t r;
-  if (e < (len / 4) * 8) {
-    const int16_t sv = (int16_t)v;
-    r = (uint16_t)((shift < 0 || shift > 15) ? (sv < 0 ? -1 : 0) : (sv >> shift));
-  } else {
-    r = (uint16_t)((shift < 0 || shift > 15) ? 0 : (v >> shift));
-  }
-  z[e] = r;
 }
 
 }  // namespace zrx
