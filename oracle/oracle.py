@@ -28,6 +28,20 @@ def build(quiet=True):
         subprocess.check_call(["make", "-C", _HERE, "-f", "Makefile.ref"], stdout=out, stderr=out)
 
 
+HOOKED_DRIVER = os.path.join(_HERE, "_ref", "driver_hooked")
+
+
+def build_hook(quiet=True):
+    """The reference's own driver (csrc/driver.cpp + runtime, from /root/reference) with the
+    batching hook of integration/csrc linked against libziria_rx.so (oracle/Makefile.hook).
+    Returns the binary's path, or None where /root/reference is absent and it was not built
+    before (a GPU box runs the binary built here)."""
+    if os.path.isdir("/root/reference/csrc"):
+        out = subprocess.DEVNULL if quiet else None
+        subprocess.check_call(["make", "-C", _HERE, "-f", "Makefile.hook"], stdout=out)
+    return HOOKED_DRIVER if os.path.exists(HOOKED_DRIVER) else None
+
+
 def lib():
     global _lib
     if _lib is None:

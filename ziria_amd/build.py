@@ -41,18 +41,20 @@ def _stale():
 
 
 DRIVER = os.path.join(LIBDIR, "ziria_rx_driver")
-DRIVER_SRC = os.path.join(HERE, "..", "tools", "ziria_rx_driver.cpp")
+DRIVER_SRC = [os.path.join(HERE, "..", "tools", "ziria_rx_driver.cpp"),
+              os.path.join(HERE, "..", "integration", "csrc", "hip_ext_batch.cpp")]
 
 
 PERCALL = os.path.join(LIBDIR, "percall_bench")
-PERCALL_SRC = os.path.join(HERE, "..", "tools", "percall_bench.cpp")
+PERCALL_SRC = [os.path.join(HERE, "..", "tools", "percall_bench.cpp")]
 
 
-def _host_tool(exe, src, verbose):
-    if os.path.exists(exe) and os.path.getmtime(exe) >= max(os.path.getmtime(src), os.path.getmtime(LIB)):
+def _host_tool(exe, srcs, verbose):
+    if os.path.exists(exe) and os.path.getmtime(exe) >= max(max(os.path.getmtime(s) for s in srcs),
+                                                            os.path.getmtime(LIB)):
         return exe
-    cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-o", exe + ".tmp", src, "-L" + LIBDIR, "-lziria_rx",
-           "-Wl,-rpath,$ORIGIN"]
+    cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-I" + os.path.join(HERE, "..", "include"), "-o", exe + ".tmp"] + \
+        list(srcs) + ["-L" + LIBDIR, "-lziria_rx", "-Wl,-rpath,$ORIGIN"]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)
@@ -62,8 +64,9 @@ def _host_tool(exe, src, verbose):
 
 def build_driver(verbose=False):
     """The host programs linked against the library (rpath $ORIGIN, next to it in
-    ziria_amd/_lib): the batching driver (tools/ziria_rx_driver.cpp) and the per-call
-    latency bench (tools/percall_bench.cpp)."""
+    ziria_amd/_lib): the standalone batching driver (tools/ziria_rx_driver.cpp around the
+    driver.cpp hook of integration/csrc/hip_ext_batch.cpp) and the per-call bench
+    (tools/percall_bench.cpp)."""
     _host_tool(PERCALL, PERCALL_SRC, verbose)
     return _host_tool(DRIVER, DRIVER_SRC, verbose)
 
