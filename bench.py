@@ -13,7 +13,8 @@ kernel of every timed step (zrx_enable_timing), so `roofline.achieved` is measur
 over the timed region.  `roofline.traffic` is the per-launch HBM byte count from the
 rocprofv3 PMC passes summarised in profiles/pmc_summary.json (scripts/pmc_summary.py).
 
-python bench.py [--gpus N --steps K --warmup W]   (N>1 under torch.distributed.run)
+python bench.py [--gpus N --steps K --warmup W]   (N>1: one process per GPU; started under
+torch.distributed.run by the caller, or by bench.py itself when WORLD_SIZE is not set)
 
 Secondary workloads (our own reporting, not the driver's line): --config 2 = BASELINE
 config 2, the batched Viterbi alone (4096 x 1500-byte frames, rate 1/2, soft input in HBM);
@@ -72,6 +73,8 @@ def main():
     ap.add_argument("--pipeline", type=int, default=2, choices=[1, 2],
                     help="batches in flight: 2 = two engines (own workspace and stream) take the steps in "
                          "turn, as a streaming receiver would, so one batch's tail overlaps the next one's head")
+    ap.add_argument("--batches", type=int, default=2,
+                    help="distinct input batches per GPU the steps rotate through (config 3/4/5)")
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 5])
     ap.add_argument("--tx", action="store_true",
                     help="TX chain (transmitter() at 40 MHz, SURVEY §8f row 4) on config-3 packets")
@@ -87,7 +90,13 @@ def main():
     if args.config == 5:
         return bench_mixed(args)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = int(os.environ.get("WORLD_SIZE", "0"))
+    if args.gpus > 1 and world == 0:
+        return spawn_ranks(args.gpus)                  # before anything touches the GPU
+    world = max(world, 1)
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
@@ -97,62 +106,88 @@ def main():
 
     # ---------------------------------------------------------------- workload (HBM-resident)
     # One global batch (BASELINE config 4): packet i depends only on (seed, i), each rank
-    # builds and decodes its contiguous shard, rank 0 checks every gathered packet.
+    # builds and decodes its contiguous shard, rank 0 checks every gathered packet.  Each rank
+    # holds args.batches distinct such batches (seeds 0x5EED + b) and the steps rotate through
+    # them, so no step re-reads samples the previous one left in the caches (MI355X's 256 MiB
+    # Infinity Cache holds a whole 239 MB batch).
     total = args.total if args.total else args.npkts * world
     sigma = 2.0 if args.eq else 4.0
+    nb = args.batches
     # args.pipeline engines, each with its own workspace and stream, take the steps in turn;
-    # every step is still one whole pass of the chain over the shard
+    # every step is still one whole pass of the chain over one batch
     engs = [RxEngine(local) for _ in range(args.pipeline)]
     streams = [torch.cuda.Stream(dev) for _ in range(args.pipeline)]
     eng = engs[0]
-    state = {"k": 0}
+    state = {}
 
     def make_shard(lo, hi):
-        b = txgen.make_batch_range(lo, hi, mod=3, coding=2, payload_len=args.payload, sigma=sigma, seed=0x5EED,
-                                   device=dev, channel=args.eq)
-        n, S = hi - lo, b["max_nsym"]
+        bs = [txgen.make_batch_range(lo, hi, mod=3, coding=2, payload_len=args.payload, sigma=sigma,
+                                     seed=0x5EED + j, device=dev, channel=args.eq) for j in range(nb)]
+        n, S = hi - lo, max(x["max_nsym"] for x in bs)
         for e in engs:
             e.reserve(max(n, 1), S)
-        b["outs"] = [(torch.zeros((n, 4096), dtype=torch.uint8, device=dev),
-                      torch.zeros((n, 8), dtype=torch.int32, device=dev)) for _ in engs]
-        b["out_payload"], b["out_info"] = b["outs"][0]
-        state["b"] = b
-        return b
+        outs = [(torch.zeros((n, 4096), dtype=torch.uint8, device=dev),
+                 torch.zeros((n, 8), dtype=torch.int32, device=dev)) for _ in engs]
+        # the engines run on their own (non-blocking) streams: order them after the inputs and
+        # the zero-filled outputs made on the current stream
+        for st in streams:
+            st.wait_stream(torch.cuda.current_stream(dev))
+        state.update(batches=bs, outs=outs, S=S, n=n)
+        return state
 
-    def run_on(j, b):
+    def run_on(j, bi):
+        x = state["batches"][bi]
         with torch.cuda.stream(streams[j]):
-            engs[j].rx(b["sym"], b["sym_off"], b["nsym"], b["max_nsym"], b["outs"][j][0], b["outs"][j][1],
-                       chan=b.get("chan"))
+            engs[j].rx(x["sym"], x["sym_off"], x["nsym"], state["S"], state["outs"][j][0], state["outs"][j][1],
+                       chan=x.get("chan"))
 
-    def step(b):
-        j = state["k"] % len(engs)
-        state["k"] += 1
-        run_on(j, b)
+    def step(sh, k):
+        run_on(k % len(engs), k % nb)
 
-    # stage times: a separate instrumented pass of engine 0 alone, after the warmup and before
-    # the timed steps (the pipelined steps overlap, so their per-stream event spans would include
-    # the other batch; the timers' own event records stay out of the timed region)
+    # stage times: a separate instrumented pass of engine 0 alone over the rotating batches,
+    # after the warmup and before the timed steps (the pipelined steps overlap, so their
+    # per-stream event spans would include the other batch; the timers' own event records
+    # stay out of the timed region)
     def instrumented(on):
         if not on:
             return
         eng.enable_timing(True)
-        for _ in range(max(3, min(args.steps, 10))):
-            run_on(0, state["b"])
+        for i in range(max(3 * nb, min(args.steps, 10))):
+            run_on(0, i % nb)
         torch.cuda.synchronize(dev)
         state["stage"] = eng.stage_ms()
         eng.enable_timing(False)
 
-    res = node.run_sharded(total, make_shard, step, lambda b: (b["out_payload"], b["out_info"]),
-                           lambda lo, hi: txgen.payloads_range(lo, hi, args.payload, seed=0x5EED),
+    # after the timed region: batch b decoded by every engine, engine 0's output returned for
+    # the per-packet check, the others compared with it
+    state["outs_equal"] = True
+
+    def outputs(sh, bi):
+        for j in range(len(engs)):
+            run_on(j, bi)
+        torch.cuda.synchronize(dev)
+        o = state["outs"]
+        state["outs_equal"] &= all(bool((x[0] == o[0][0]).all()) and bool((x[1] == o[0][1]).all()) for x in o[1:])
+        return o[0]
+
+    res = node.run_sharded(total, make_shard, step, outputs,
+                           lambda lo, hi, bi: txgen.payloads_range(lo, hi, args.payload, seed=0x5EED + bi),
                            args.steps, args.warmup, args.payload, device=dev, crc_ok_only=args.eq,
-                           on_timed=instrumented)
-    b = state["b"]
+                           on_timed=instrumented, nbatches=nb)
     stage = state["stage"]
-    torch.cuda.synchronize(dev)
-    outs_equal = all(bool((o[0] == b["outs"][0][0]).all()) and bool((o[1] == b["outs"][0][1]).all())
-                     for o in b["outs"][1:])
-    n, S = res["hi"] - res["lo"], b["max_nsym"]
+    n, S = res["hi"] - res["lo"], state["S"]
     elapsed = res["elapsed"]
+
+    # the same K steps with engine 0 alone (one batch in flight): the pipelined value above is
+    # not a kernel speed-up, this is what the overlap of two batches adds to
+    torch.cuda.synchronize(dev)
+    node.barrier(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        run_on(0, k % nb)
+    torch.cuda.synchronize(dev)
+    node.barrier(dev)
+    single = node.max_over_ranks(time.perf_counter() - t0, device=dev)
 
     decoded_bits = n * (args.payload + 4 + 2) * 8          # Viterbi output bits per launch (this rank)
     vit_ms = stage["data_viterbi"]
@@ -164,10 +199,10 @@ def main():
     value = res["bits"] * args.steps / elapsed / 1e6       # CRC-checked payload bits, all ranks
     ms_per_step = elapsed / args.steps * 1e3
 
-    # ---------------------------------------------------------------- CPU baseline (rank 0, N=1)
+    # ---------------------------------------------------------------- CPU baseline (rank 0)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(b, args.cpu_seconds, b.get("chan"))
+    if rank == 0 and not args.no_cpu:
+        cpu = cpu_baseline(state["batches"][0], args.cpu_seconds, state["batches"][0].get("chan"))
 
     if rank == 0:
         line = {
@@ -183,7 +218,8 @@ def main():
             "vs_baseline": None,
             "dtype": "int16+u8",
             "data": ("synthetic (txgen.make_batch_range: random payloads, TX restated from transmitter.blk, "
-                     + ("3-tap channel + phase drift, AWGN sigma=2)" if args.eq else "AWGN sigma=4)")),
+                     + ("3-tap channel + phase drift, AWGN sigma=2" if args.eq else "AWGN sigma=4")
+                     + f"; {nb} distinct batches per GPU, the steps rotate through them)"),
             "config": {"workload": f"config{'3+eq' if args.eq else ('4' if world > 1 else '3')}: {total} packets "
                                    f"({n} per GPU, contiguous shards) x {args.payload} B payload "
                                    f"@ 54 Mbps (64-QAM r3/4), {S} CP-removed complex16 OFDM symbols each, "
@@ -191,14 +227,18 @@ def main():
                                    + (", FFT >>> ChannelEqualization >>> PilotTrack >>> GetData" if args.eq else ""),
                        "packets_total": total, "packets_per_gpu": n, "payload_bytes": args.payload,
                        "symbols_per_packet": S, "parallelism": f"packet-sharded x{world}",
+                       "batches_per_gpu": nb,
                        "pipeline": f"{len(engs)} batches in flight (engines on separate streams, steps in turn)"},
+            "value_one_engine": round(res["bits"] * args.steps / single / 1e6, 1),
             "bit_exact_check": {"crc_pass": res["ok"], "packets": res["packets"],
                                 "payload_match": res["payload_match"],
                                 "mismatched_packets": res["mismatched_packets"],
-                                "pipeline_outputs_equal": outs_equal,
-                                "checked_on": "rank 0, every gathered packet vs its transmitted payload"},
+                                "pipeline_outputs_equal": state["outs_equal"],
+                                "checked_on": f"rank 0, every gathered packet of all {nb} batches vs its "
+                                              "transmitted payload"},
             "stage_ms": {k: round(v, 4) for k, v in stage.items()},
-            "stage_ms_from": "engine 0 alone, HIP events, after the warmup and before the timed steps",
+            "stage_ms_from": "engine 0 alone over the rotating batches, HIP events, after the warmup and before "
+                             "the timed steps",
             "roofline": {"kernel": "k_viterbi3 (data Viterbi)", "bound": "valu",
                          "achieved": round(achieved_tops, 3), "peak": round(VALU_PEAK_TOPS, 1),
                          "unit": "Tops/s", "frac": round(achieved_tops / VALU_PEAK_TOPS, 4),
@@ -215,6 +255,26 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` without a launcher: runs this script again under
+    torch.distributed.run, one process per GPU on this node (rendezvous on 127.0.0.1), as a
+    child process (no exec: nothing here has touched the GPU yet, and the child re-parses the
+    same arguments).  Returns the launcher's exit code, non-zero if any rank failed."""
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(sys.argv[0])] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    rc = subprocess.call(cmd, env=env)
+    if rc:
+        print(f"bench.py: torch.distributed.run with {n} ranks exited with {rc}", file=sys.stderr)
+    sys.exit(rc)
 
 
 def _timed(step, steps, warmup):
@@ -292,16 +352,19 @@ def bench_viterbi_only(args):
 
 
 def bench_mixed(args):
-    """BASELINE config 5: mixed MCS batch through the whole chain, every packet distinct
-    (txgen.make_mixed_fast); every CRC-passing payload is checked against what was sent and
-    a sample against the oracle."""
+    """BASELINE config 5: mixed MCS batches through the whole chain, every packet distinct
+    (txgen.make_mixed_fast); args.batches distinct batches, the steps rotate through them.
+    Every CRC-passing payload of every batch is checked against what was sent and a sample of
+    batch 0 against the oracle."""
     from oracle import oracle as O
     dev = torch.device("cuda", 0)
     n = args.npkts                                       # 16384, as config 3
+    nb = args.batches
     tg = time.perf_counter()
-    m = txgen.make_mixed_fast(n, min_len=64, max_len=4095, sigma=3.0, seed=0x3C5, device=dev)
+    ms = [txgen.make_mixed_fast(n, min_len=64, max_len=4095, sigma=3.0, seed=0x3C5 + j, device=dev)
+          for j in range(nb)]
     gen_s = time.perf_counter() - tg
-    S = m["max_nsym"]
+    S = max(m["max_nsym"] for m in ms)
     # args.pipeline engines (own workspace and stream) take the steps in turn, as in main()
     engs = [RxEngine(0) for _ in range(args.pipeline)]
     streams = [torch.cuda.Stream(dev) for _ in engs]
@@ -310,41 +373,56 @@ def bench_mixed(args):
         e.reserve(n, S)
         outs.append((torch.zeros((n, 4096), dtype=torch.uint8, device=dev),
                      torch.zeros((n, 8), dtype=torch.int32, device=dev)))
+    for st in streams:                                   # inputs and outputs come from the current stream
+        st.wait_stream(torch.cuda.current_stream(dev))
     eng = engs[0]
-    payload, info = outs[0]
     k = {"i": 0}
 
-    def run_on(j):
+    def run_on(j, bi):
+        m = ms[bi]
         with torch.cuda.stream(streams[j]):
             engs[j].rx(m["sym"], m["sym_off"], m["nsym"], S, outs[j][0], outs[j][1])
 
     def step():
-        run_on(k["i"] % len(engs))
+        run_on(k["i"] % len(engs), k["i"] % nb)
         k["i"] += 1
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     eng.enable_timing(True)                              # stage times: engine 0 alone, before the timed steps
-    for _ in range(max(3, min(args.steps, 10))):
-        run_on(0)
+    for i in range(max(3 * nb, min(args.steps, 10))):
+        run_on(0, i % nb)
     torch.cuda.synchronize()
     stage = eng.stage_ms()
     eng.enable_timing(False)
+    first = k["i"]
     elapsed = _timed(step, args.steps, 0)
-    outs_equal = all(bool((o[0] == payload).all()) and bool((o[1] == info).all()) for o in outs[1:])
-    inf = info.cpu().numpy()
-    pay = payload.cpu().numpy()
-    ok = inf[:, 4] == 1
-    good = all((pay[i, :len(m["payload"][i])] == m["payload"][i]).all() for i in range(n) if ok[i])
-    expect_ok = int((m["meta"][:, 2] <= 2048).sum())
-    bits = int(((inf[:, 2] - 4) * 8 * ok).sum())
+    timed_batches = [(first + i) % nb for i in range(args.steps)]
+    # every batch decoded once more by every engine: per-packet checks, engines compared
+    outs_equal, good, crc_pass, expect_ok, bits_b, infos, pays = True, True, 0, 0, [], [], []
+    for bi, m in enumerate(ms):
+        for j in range(len(engs)):
+            run_on(j, bi)
+        torch.cuda.synchronize()
+        outs_equal &= all(bool((o[0] == outs[0][0]).all()) and bool((o[1] == outs[0][1]).all()) for o in outs[1:])
+        inf = outs[0][1].cpu().numpy()
+        pay = outs[0][0].cpu().numpy()
+        ok = inf[:, 4] == 1
+        good &= all((pay[i, :len(m["payload"][i])] == m["payload"][i]).all() for i in range(n) if ok[i])
+        crc_pass += int(ok.sum())
+        expect_ok += int((m["meta"][:, 2] <= 2048).sum())
+        bits_b.append(int(((inf[:, 2] - 4) * 8 * ok).sum()))
+        infos.append(inf)
+        pays.append(pay)
+    bits = sum(bits_b[bi] for bi in timed_batches) / args.steps
     threads, host = host_cpus()
     sample = min(1024, n)
-    soff, sn = m["sym_off"][:sample].cpu().numpy(), m["nsym"][:sample].cpu().numpy()
-    sym_s = m["sym"][:int((soff + sn).max())].cpu().numpy()
+    m0, inf, pay = ms[0], infos[0], pays[0]
+    soff, sn = m0["sym_off"][:sample].cpu().numpy(), m0["nsym"][:sample].cpu().numpy()
+    sym_s = m0["sym"][:int((soff + sn).max())].cpu().numpy()
     opay, res = O.rx_batch_time(sym_s, soff, sn, nthreads=threads)
-    cpu = cpu_baseline(m, args.cpu_seconds)
+    cpu = cpu_baseline(m0, args.cpu_seconds)
     oracle_match = all(int(inf[i, 4]) == r["crc_ok"] and int(inf[i, 2]) == r["len"] and
                        (not r["crc_ok"] or (pay[i, :r["len"] - 4] == opay[i, :r["len"] - 4]).all())
                        for i, r in enumerate(res))
@@ -353,12 +431,13 @@ def bench_mixed(args):
         "value": round(bits * args.steps / elapsed / 1e6, 1), "unit": "Mbit/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int16+u8",
-        "data": f"synthetic (txgen.make_mixed_fast: {n} distinct packets, 8 MCS, PSDU 64..4095 B, AWGN sigma=3; "
-                f"generated in {gen_s:.1f} s)",
-        "config": {"workload": f"config5: {n} packets, {S} symbols max, {int(m['nsym'].sum())} symbols"},
-        "bit_exact_check": {"crc_pass": int(ok.sum()), "expected_crc_pass": expect_ok, "payload_match": good,
+        "data": f"synthetic (txgen.make_mixed_fast: {nb} batches of {n} distinct packets, 8 MCS, PSDU 64..4095 B, "
+                f"AWGN sigma=3; generated in {gen_s:.1f} s; the steps rotate through the batches)",
+        "config": {"workload": f"config5: {n} packets per batch, {S} symbols max, "
+                               f"{int(ms[0]['nsym'].sum())} symbols in batch 0", "batches": nb},
+        "bit_exact_check": {"crc_pass": crc_pass, "expected_crc_pass": expect_ok, "payload_match": good,
                             "oracle_sample": sample, "oracle_sample_match": bool(oracle_match),
-                            "pipeline_outputs_equal": outs_equal},
+                            "pipeline_outputs_equal": outs_equal, "checked": f"every packet of all {nb} batches"},
         "pipeline": f"{len(engs)} batches in flight (engines on separate streams, steps in turn)",
         "stage_ms": {k: round(v, 4) for k, v in stage.items()},
         "cpu_baseline": cpu,

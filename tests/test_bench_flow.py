@@ -1,8 +1,10 @@
-"""bench.py's control flow on the CPU: main() (config 3) and bench_mixed() (config 5) with two
-batches in flight, run in a subprocess with torch.cuda stubbed and the engine replaced by a
-host decoder (the CPU port, identical to the oracle).  Checks the JSON line's bit-exactness
-fields and the order of work: warmup steps alternating engines, then the instrumented
-stage-timer pass on engine 0 alone, then exactly K timed steps alternating engines."""
+"""bench.py's control flow on the CPU: main() (configs 3 and 4) and bench_mixed() (config 5)
+with two batches in flight, run in a subprocess with torch.cuda stubbed and the engine
+replaced by a host decoder (the CPU port, identical to the oracle).  Checks the JSON line's
+bit-exactness fields and the order of work: the streams ordered after the inputs, warmup
+steps alternating engines and input batches, the instrumented stage-timer pass on engine 0
+alone, exactly K timed steps, the per-batch verification passes and the single-engine pass;
+and `bench.py --gpus 2` starting two ranks itself (gloo in place of RCCL)."""
 import json
 import os
 import subprocess
@@ -14,21 +16,36 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 HARNESS = textwrap.dedent("""
-    import contextlib, json, sys, types
+    import contextlib, json, os, sys, types
     import torch
+    import torch.distributed as dist
     sys.path.insert(0, ROOT)
+    argv = sys.argv[1:]
     sys.argv = ["bench.py"]
     import bench
     from ziria_amd import txgen
     from oracle import oracle as O
     cpu = torch.device("cpu")
+    log = []
+
+    class Stream:
+        def __init__(self, *a, **k):
+            self.id = len([x for x in log if x[0] == "stream"])
+            log.append(("stream", self.id))
+        def wait_stream(self, other):
+            log.append(("wait_stream", self.id))
+
     torch.cuda.set_device = lambda *a, **k: None
     torch.cuda.synchronize = lambda *a, **k: None
-    torch.cuda.Stream = lambda *a, **k: object()
+    torch.cuda.Stream = Stream
+    torch.cuda.current_stream = lambda *a, **k: "current"
     torch.cuda.stream = lambda s: contextlib.nullcontext()
     bench.torch = types.SimpleNamespace(**{k: getattr(torch, k) for k in dir(torch) if not k.startswith("__")})
     bench.torch.device = lambda *a, **k: cpu
-    log = []
+    init = dist.init_process_group
+    bench.dist = types.SimpleNamespace(**{k: getattr(dist, k) for k in dir(dist) if not k.startswith("__")})
+    bench.dist.init_process_group = lambda *a, **k: init("gloo")
+    batches = {}
 
     class Engine:
         def __init__(self, dev):
@@ -42,45 +59,83 @@ HARNESS = textwrap.dedent("""
             return dict(signal_fft=0.01, signal_viterbi=0.03, data_fft_demap=0.13, data_viterbi=1.25,
                         descramble_crc=0.03)
         def rx(self, sym, off, nsym, S, payload, info, chan=None):
-            log.append(("rx", self.id))
+            b = batches.setdefault(sym.data_ptr(), len(batches))
+            log.append(("rx", self.id, b))
             pay, res = O.rx_batch_time_fast(sym.numpy(), off.numpy(), nsym.numpy(), nthreads=4)
             payload[:] = torch.from_numpy(pay)
             for i, r in enumerate(res):
                 info[i, :5] = torch.tensor([r["modulation"], r["coding"], r["len"], r["err"], r["crc_ok"]])
 
     bench.RxEngine = Engine
-    make = txgen.make_batch_range
+    make, mixed = txgen.make_batch_range, txgen.make_mixed_fast
     bench.txgen = types.SimpleNamespace(**{k: getattr(txgen, k) for k in dir(txgen) if not k.startswith("__")})
     bench.txgen.make_batch_range = lambda lo, hi, **k: make(lo, hi, **{**k, "device": cpu})
-    sys.argv = ["bench.py"] + ARGS
+    bench.txgen.make_mixed_fast = lambda n, **k: mixed(n, **{**k, "device": cpu})
+    sys.argv = [os.path.abspath(__file__)] + argv
     bench.main()
-    print("LOG " + json.dumps(log))
+    print("LOG %s %s" % (os.environ.get("RANK", "0"), json.dumps(log)), flush=True)
 """)
 
 
-def _run(args):
-    code = f"ROOT = {ROOT!r}\nARGS = {args!r}\n" + HARNESS
-    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=600, cwd=ROOT)
-    assert p.returncode == 0, p.stderr[-3000:]
+def _run(tmp_path, args):
+    script = tmp_path / "bench_harness.py"
+    script.write_text(f"ROOT = {ROOT!r}\n" + HARNESS)
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, str(script)] + args, capture_output=True, text=True, timeout=900, cwd=ROOT,
+                       env=env)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     lines = p.stdout.splitlines()
     line = json.loads(next(x for x in lines if x.startswith("{")))
-    log = json.loads(next(x for x in lines if x.startswith("LOG "))[4:])
-    return line, log
+    logs = {}
+    for x in lines:
+        if x.startswith("LOG "):
+            rank, js = x[4:].split(" ", 1)
+            logs[int(rank)] = json.loads(js)
+    return line, logs
 
 
 @pytest.mark.parametrize("args,k,w", [
     (["--npkts", "24", "--steps", "4", "--warmup", "2", "--no-cpu"], 4, 2),
     (["--config", "5", "--npkts", "40", "--steps", "3", "--warmup", "1", "--cpu-seconds", "0.2"], 3, 1),
 ])
-def test_bench_pipelined_flow(oracle, args, k, w):
-    line, log = _run(args)
+def test_bench_pipelined_flow(oracle, tmp_path, args, k, w):
+    line, logs = _run(tmp_path, args)
+    log = logs[0]
     b = line["bit_exact_check"]
     assert b["payload_match"] is True and b["pipeline_outputs_equal"] is True
     assert line["steps"] == k and line["warmup"] == w and "2 batches in flight" in str(line)
+    nb = 2
+    # both engine streams wait for the current stream before the first launch
+    first_rx = next(i for i, e in enumerate(log) if e[0] == "rx")
+    assert sorted(e[1] for e in log[:first_rx] if e[0] == "wait_stream") == [0, 1]
     rx = [e for e in log if e[0] in ("rx", "timing")]
     on = rx.index(["timing", True])
     off = rx.index(["timing", False])
-    warm, inst, timed = rx[:on], rx[on + 1:off], rx[off + 1:]
-    assert [e[1] for e in warm] == [i % 2 for i in range(w)]
-    assert inst and all(e == ["rx", 0] for e in inst)
-    assert [e[1] for e in timed] == [(w + i) % 2 for i in range(k)]
+    warm, inst, rest = rx[:on], rx[on + 1:off], rx[off + 1:]
+    assert [e[1:] for e in warm] == [[i % 2, i % nb] for i in range(w)]
+    assert len(inst) >= 3 * nb and all(e[1] == 0 for e in inst) and sorted({e[2] for e in inst}) == [0, 1]
+    timed, verify = rest[:k], rest[k:k + 2 * nb]
+    assert [e[1:] for e in timed] == [[(w + i) % 2, (w + i) % nb] for i in range(k)]
+    assert [e[1:] for e in verify] == [[j, bi] for bi in range(nb) for j in range(2)]
+    if "--config" not in args:                      # config 3: the single-engine pass, K steps on engine 0
+        single = rest[k + 2 * nb:]
+        assert [e[1:] for e in single] == [[0, i % nb] for i in range(k)]
+        assert line["config"]["batches_per_gpu"] == nb and b["packets"] == nb * 24
+        assert line["value_one_engine"] > 0
+
+
+def test_bench_gpus2_spawns_two_ranks(oracle, tmp_path):
+    """`bench.py --gpus 2` with no launcher starts two ranks itself (torch.distributed.run as a
+    child); rank 0 gathers every packet of both ranks' shards and prints one line for 2 GPUs,
+    with the CPU baseline."""
+    line, logs = _run(tmp_path, ["--gpus", "2", "--npkts", "12", "--steps", "2", "--warmup", "1",
+                                 "--cpu-seconds", "0.2"])
+    assert sorted(logs) == [0, 1]
+    assert line["n_gpus"] == 2 and line["config"]["packets_total"] == 24 and line["config"]["packets_per_gpu"] == 12
+    b = line["bit_exact_check"]
+    assert b["packets"] == 2 * 24 and b["crc_pass"] == 2 * 24 and b["payload_match"] is True
+    assert b["mismatched_packets"] == 0
+    assert line["cpu_baseline"]["value"] > 0
+    for r in (0, 1):
+        assert any(e[0] == "rx" for e in logs[r])

@@ -89,8 +89,8 @@ def test_combine_over_gloo(world, npkts):
 L = 24
 
 
-def _payload(lo, hi):
-    return ((torch.arange(lo, hi).unsqueeze(1) * 7 + torch.arange(L)) % 251).to(torch.uint8).numpy()
+def _payload(lo, hi, b=0):
+    return ((torch.arange(lo, hi).unsqueeze(1) * 7 + torch.arange(L) + 13 * b) % 251).to(torch.uint8).numpy()
 
 
 def _bench_worker(rank, world, port, total, corrupt, out):
@@ -100,24 +100,32 @@ def _bench_worker(rank, world, port, total, corrupt, out):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        calls = {"step": 0}
+        calls = {"step": [], "verify": []}
 
         def make_shard(lo, hi):
             return {"lo": lo, "hi": hi, "pay": torch.zeros((hi - lo, 64), dtype=torch.uint8),
                     "info": torch.zeros((hi - lo, 8), dtype=torch.int32)}
 
-        def step(sh):
-            calls["step"] += 1
-            sh["pay"][:, :L] = torch.from_numpy(_payload(sh["lo"], sh["hi"]))
-            if corrupt and sh["lo"] <= 5 < sh["hi"]:
+        def decode(sh, b):
+            sh["pay"][:, :L] = torch.from_numpy(_payload(sh["lo"], sh["hi"], b))
+            if corrupt and b == 1 and sh["lo"] <= 5 < sh["hi"]:
                 sh["pay"][5 - sh["lo"], 3] ^= 1
             sh["info"][:, 2] = L + 4
             sh["info"][:, 4] = 1
 
+        def step(sh, k):
+            calls["step"].append(k)
+            decode(sh, k % 2)
+
+        def outputs(sh, b):
+            calls["verify"].append(b)
+            decode(sh, b)
+            return sh["pay"], sh["info"]
+
         timed = []
-        res = node.run_sharded(total, make_shard, step, lambda sh: (sh["pay"], sh["info"]), _payload,
-                               steps=3, warmup=2, payload_len=L, on_timed=timed.append)
-        out.put((rank, res["lo"], res["hi"], calls["step"], timed, res["ok"], res["bits"],
+        res = node.run_sharded(total, make_shard, step, outputs, _payload,
+                               steps=3, warmup=2, payload_len=L, on_timed=timed.append, nbatches=2)
+        out.put((rank, res["lo"], res["hi"], calls, timed, res["ok"], res["bits"],
                  res.get("packets"), res.get("payload_match"), res.get("mismatched_packets")))
     finally:
         dist.destroy_process_group()
@@ -138,10 +146,11 @@ def test_run_sharded_over_gloo(world, total, corrupt):
     ranges = [(g[1], g[2]) for g in got]
     assert ranges == [node.shard_range(total, world, r) for r in range(world)]
     for g in got:
-        assert g[3] == 5 and g[4] == [True, False]          # 2 warmup + 3 timed steps, timers on/off
-        assert g[5] == total and g[6] == total * L * 8      # summed over ranks
+        assert g[3] == {"step": [0, 1, 2, 3, 4], "verify": [0, 1]}   # 2 warmup + 3 timed steps, both batches checked
+        assert g[4] == [True, False]                                # timers on / off
+        assert g[5] == 2 * total and g[6] == total * L * 8          # summed over ranks (CRC passes of both batches)
     r0 = got[0]
-    assert r0[7] == total
+    assert r0[7] == 2 * total
     assert r0[8] is (not corrupt)
     assert r0[9] == (1 if corrupt else 0)
 
@@ -149,5 +158,6 @@ def test_run_sharded_over_gloo(world, total, corrupt):
 def test_run_sharded_single_process():
     res = node.run_sharded(5, lambda lo, hi: {"p": torch.from_numpy(_payload(lo, hi)),
                                               "i": torch.ones((hi - lo, 8), dtype=torch.int32) * 0 + torch.tensor([0, 0, L + 4, 0, 1, 0, 0, 0], dtype=torch.int32)},
-                           lambda sh: None, lambda sh: (sh["p"], sh["i"]), _payload, steps=1, warmup=0, payload_len=L)
+                           lambda sh, k: None, lambda sh, b: (sh["p"], sh["i"]), _payload, steps=1, warmup=0,
+                           payload_len=L)
     assert (res["lo"], res["hi"], res["ok"], res["packets"], res["payload_match"]) == (0, 5, 5, 5, True)

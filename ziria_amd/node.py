@@ -107,25 +107,32 @@ def _sync(device):
 
 
 def run_sharded(total, make_shard, step, outputs, expected, steps, warmup, payload_len, device=None,
-                crc_ok_only=False, on_timed=None):
+                crc_ok_only=False, on_timed=None, nbatches=1):
     """The bench's N-rank loop over one global batch of `total` packets.
 
-    make_shard(lo, hi) builds this rank's packets [lo, hi) (already in device memory);
-    step(shard) runs one decode of the shard; outputs(shard) -> (payload uint8 [n, >=L],
-    info int32 [n, 8]) of the last step; expected(lo, hi) -> uint8 numpy [hi-lo, L], the
-    transmitted payloads (L = payload_len bytes each), which rank 0 uses to check every
-    gathered packet.
+    make_shard(lo, hi) builds this rank's packets [lo, hi) (already in device memory) as
+    `nbatches` distinct batches of the same shape (a streaming receiver never decodes the same
+    samples twice, so the timed steps rotate through them); step(shard, k) runs decode step k
+    (k counts from 0 over the warmup and timed steps: bench.py decodes batch k % nbatches);
+    outputs(shard, b) -> (payload uint8 [n, >=L], info int32 [n, 8]) of batch b, decoded once
+    more after the timed region; expected(lo, hi, b) -> uint8 numpy [hi-lo, L], the
+    transmitted payloads of batch b (L = payload_len bytes each), which rank 0 uses to check
+    every gathered packet of every batch.
     on_timed(True) is called after the warmup, before the barrier that opens the timed region
     (bench.py runs its instrumented stage-timer pass there), on_timed(False) after it closes.
 
     Timing: `warmup` untimed steps, then barrier + device sync, `steps` timed steps, device
     sync + barrier, and the slowest rank's time.  Returns on every rank a dict with the
-    shard, the timing and the combined counts; rank 0's also holds the per-packet check."""
+    shard, the timing and the combined counts (`bits` = CRC-checked payload bits per timed
+    step, all ranks: the mean over the batches the timed steps decoded); rank 0's also holds
+    the per-packet check over all batches."""
     world, rank = world_rank()
     lo, hi = shard_range(total, world, rank)
     shard = make_shard(lo, hi)
+    k = 0
     for _ in range(warmup):
-        step(shard)
+        step(shard, k)
+        k += 1
     _sync(device)
     if on_timed:
         on_timed(True)
@@ -133,8 +140,11 @@ def run_sharded(total, make_shard, step, outputs, expected, steps, warmup, paylo
     barrier(device)
     _sync(device)
     t0 = time.perf_counter()
+    timed_batches = []
     for _ in range(steps):
-        step(shard)
+        step(shard, k)
+        timed_batches.append(k % nbatches)
+        k += 1
     _sync(device)
     barrier(device)
     t1 = time.perf_counter()
@@ -142,24 +152,38 @@ def run_sharded(total, make_shard, step, outputs, expected, steps, warmup, paylo
         on_timed(False)
     elapsed = max_over_ranks(t1 - t0, device=device)
 
-    payload, info = outputs(shard)
     L = payload_len
-    ok, bits, _ = counts(info)
-    _sync(device)
-    tg = time.perf_counter()
-    ok_all, bits_all, _, pay_all = combine(ok, bits, 1, payload[:, :L].contiguous(), device=device)
-    info_all = gather_rows(info.contiguous())
-    _sync(device)
-    gather_s = time.perf_counter() - tg
-    res = dict(lo=lo, hi=hi, shard=shard, elapsed=elapsed, steps=steps, ok=ok_all, bits=bits_all,
-               gather_s=gather_s, world=world, rank=rank)
+    ok_b, bits_b, pay_b, info_b = [], [], [], []
+    gather_s = 0.0
+    for b in range(nbatches):
+        payload, info = outputs(shard, b)
+        ok, bits, _ = counts(info)
+        _sync(device)
+        tg = time.perf_counter()
+        ok_all, bits_all, _, pay_all = combine(ok, bits, 1, payload[:, :L].contiguous(), device=device)
+        info_all = gather_rows(info.contiguous())
+        _sync(device)
+        gather_s += time.perf_counter() - tg
+        ok_b.append(ok_all)
+        bits_b.append(bits_all)
+        pay_b.append(pay_all)
+        info_b.append(info_all)
+    bits_per_step = sum(bits_b[b] for b in timed_batches) / max(steps, 1)
+    res = dict(lo=lo, hi=hi, shard=shard, elapsed=elapsed, steps=steps, ok=sum(ok_b), bits=bits_per_step,
+               bits_per_batch=bits_b, gather_s=gather_s / max(nbatches, 1), world=world, rank=rank, batches=nbatches)
     if rank == 0:
-        pay = pay_all.cpu().numpy()
-        inf = info_all.cpu().numpy()
-        exp = np.asarray(expected(0, total))
-        crc = inf[:, 4] == 1
-        same = (pay[:, :exp.shape[1]] == exp).all(axis=1)
-        res["packets"] = int(pay.shape[0])
-        res["payload_match"] = bool(same[crc].all() if crc_ok_only else same.all())
-        res["mismatched_packets"] = int((~same & (crc if crc_ok_only else True)).sum())
+        packets = mism = 0
+        match = True
+        for b in range(nbatches):
+            pay = pay_b[b].cpu().numpy()
+            inf = info_b[b].cpu().numpy()
+            exp = np.asarray(expected(0, total, b))
+            crc = inf[:, 4] == 1
+            same = (pay[:, :exp.shape[1]] == exp).all(axis=1)
+            packets += int(pay.shape[0])
+            match &= bool(same[crc].all() if crc_ok_only else same.all())
+            mism += int((~same & (crc if crc_ok_only else True)).sum())
+        res["packets"] = packets
+        res["payload_match"] = match
+        res["mismatched_packets"] = mism
     return res
