@@ -648,7 +648,8 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
   }
   if (ev) ZRX_CHECK(hipEventRecord(ev[2], s));
   // k_data_fft: waves over the batch's data symbols, at most npkts x (max_nsym - 1) of them
-  const int fft_blocks = (int)std::min<int64_t>(((int64_t)npkts * (max_nsym - 1) + 255) / 256, kDataFftBlocks);
+  const int fft_blocks = (int)std::min<int64_t>(((int64_t)npkts * (max_nsym - 1) + 255) / 256,
+                                                (int64_t)kDfBlocksPerCu * c->ncu);
   if (fft_blocks > 0) {
     if (chan)
       k_data_fft<true><<<fft_blocks, 256, 0, s>>>((const uint4*)d_sym, d_sym_off, c->vparams, npkts, (uint4*)c->soft,

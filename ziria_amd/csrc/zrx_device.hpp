@@ -134,10 +134,10 @@ __device__ __forceinline__ void demap_deinterleave(const s2* x, const uint32_t* 
 }
 
 // demap_deinterleave that hands each group of 4 words (16 soft bytes) to st(q, uint4) as
-// soon as it is built, so the whole soft symbol never has to be live in registers
-// (k_data_fft: 159 -> fewer VGPRs, more resident waves per SIMD).
-template <int MOD, class St>
-__device__ __forceinline__ void demap_deinterleave_st(const s2* x, const uint32_t* lut, St st) {
+// soon as it is built, so the whole soft symbol never has to be live in registers.
+// lut(i) returns kDemapLut[i] (k_data_fft reads one of several LDS copies per lane).
+template <int MOD, class Lut, class St>
+__device__ __forceinline__ void demap_deinterleave_st(const s2* x, Lut lut, St st) {
   constexpr int NB = ModInfo<MOD>::nb, NC = ModInfo<MOD>::ncbps;
   uint32_t lr[48], li[48];
 #pragma unroll
@@ -145,8 +145,8 @@ __device__ __forceinline__ void demap_deinterleave_st(const s2* x, const uint32_
     s2 v = x[bitrev6(data_bin(i))];
     v = __builtin_elementwise_max(__builtin_elementwise_min(v, (s2){127, 127}), (s2){-128, -128});
     const uint32_t u = as_u32(v);
-    lr[i] = lut[u & 0xFF];
-    li[i] = (MOD == 0) ? 0u : lut[(u >> 16) & 0xFF];
+    lr[i] = lut(u & 0xFF);
+    li[i] = (MOD == 0) ? 0u : lut((u >> 16) & 0xFF);
   }
 #pragma unroll
   for (int q = 0; q < NC / 16; q++) {

@@ -464,17 +464,35 @@ __global__ __launch_bounds__(1024) void k_pkt_rows(const int32_t* __restrict__ v
   plan_rows_mixed(vparams, npkts, Lm, rows, nrows, segs, order, out_bits, ncu, rows_cap, hist, &rtotal);
 }
 
-constexpr int kDataFftBlocks = 2048;  // k_data_fft grid cap: 8192 waves, 32 per CU, looping
+// ---- k_data_fft: FFT64 + GetData + DemapLimit + Demap + Deinterleave, lane = data symbol ----
+// The FFT runs one symbol per lane (no cross-lane traffic), but a lane's 256-B symbol and its
+// 288-B soft row are a poor memory pattern: 64 rows per load or store instruction.  So each
+// wave moves its 64 symbols through its own LDS region in both directions:
+//  * in: 16 LDS-DMA loads (global_load_lds_dwordx4), each 1 KiB of 4 whole symbols.  The
+//    destination of a DMA load is lane-linear, so the skew sits on the source: LDS unit
+//    16s + ((c + s) mod 16) holds 16-B chunk c of symbol s, and lane s's 16 ds_read_b128 of
+//    chunk c land on 16 distinct 16-B slots in every lane group (conflict-free).
+//  * out: the demapper writes unit q of the soft row to 19s + q (stride 19: 8-lane groups of
+//    ds_write_b128 hit 8 slots), then 18 store instructions each take 64 consecutive units of
+//    the wave's rows (s, q) = divmod(64j + lane, 18), i.e. 1 KiB runs of consecutive rows.
+// A wave never waits on another: LDS is in order within a wave, so there are no barriers.
+constexpr int kDfWaves = 4;           // waves per block
+constexpr int kDfRow = 19;            // output staging row stride, 16-B units (a soft row is <= 18)
+constexpr int kDfStage = 64 * kDfRow; // units per wave (>= 1024 units of input)
+constexpr int kDfLutCopies = 4;       // demap LUT copies (lane & 3): fewer LDS bank conflicts
+constexpr int kDfBlocksPerCu = 2;     // 2 x 80 KiB of LDS
+
+template <int MOD>
+__host__ __device__ constexpr int soft_units() { return ModInfo<MOD>::ncbps / 16; }
+__device__ __forceinline__ int soft_units_of(int mod) { return mod == 0 ? 3 : mod == 1 ? 6 : mod == 2 ? 12 : 18; }
 
 template <int MOD, bool EQ>
-__device__ __forceinline__ void data_fft_symbol(const uint4* __restrict__ src, int k, const uint32_t* lut,
-                                                uint4* __restrict__ dst, const uint32_t* __restrict__ cp,
-                                                const EqTabs& T) {
-  s2 x[64];
-  load_symbol(src, x);
+__device__ __forceinline__ void data_fft_symbol(s2* x, int k, const uint32_t* lut, uint4* row,
+                                                const uint32_t* __restrict__ cp, const EqTabs& T) {
   fft64_inplace(x);
   if constexpr (EQ) equalize_data_bins(x, [cp](int b) { return as_s2(cp[b]); }, k + 1, T);
-  demap_deinterleave_st<MOD>(x, lut, [dst](int q, uint4 v) { dst[q] = v; });
+  demap_deinterleave_st<MOD>(x, [lut](uint32_t i) { return lut[i * kDfLutCopies]; },
+                             [row](int q, uint4 v) { row[q] = v; });
 }
 // Flat over the batch's data symbols (k_pkt_plan numbers them): wave w takes symbols
 // 64w .. 64w+63, lane = symbol, whatever packets they belong to, so a long packet spreads
@@ -486,27 +504,67 @@ __global__ __launch_bounds__(256) void k_data_fft(const uint4* __restrict__ sym,
                                                   uint4* __restrict__ soft, const int64_t* __restrict__ soft_off,
                                                   const int32_t* __restrict__ dsym, const int32_t* __restrict__ wave_p0,
                                                   const uint32_t* __restrict__ chan, EqTabs T) {
-  __shared__ uint32_t lut[256];
-  stage_lut(lut);
+  __shared__ uint4 stage_all[kDfWaves][kDfStage];
+  __shared__ uint32_t lut_all[256 * kDfLutCopies];
+  for (int i = threadIdx.x; i < 256 * kDfLutCopies; i += blockDim.x) lut_all[i] = kDemapLut[i / kDfLutCopies];
+  __syncthreads();
   const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint4* stage = stage_all[wv];
+  const uint32_t* lut = lut_all + (lane & (kDfLutCopies - 1));
+  const char* symb = (const char*)sym;
   const int total = dsym[npkts];
   const int nw = (total + 63) >> 6;
-  for (int w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); w < nw; w += gridDim.x * 4) {
+  for (int w = __builtin_amdgcn_readfirstlane(blockIdx.x * kDfWaves + wv); w < nw; w += gridDim.x * kDfWaves) {
     const int g = w * 64 + lane;
-    if (g >= total) continue;
+    const bool valid = g < total;
     int p = wave_p0[w];
-    while (dsym[p + 1] <= g) p++;                    // packets of fewer than 64 symbols
+    if (valid)
+      while (dsym[p + 1] <= g) p++;                  // packets of fewer than 64 symbols
     const int k = g - dsym[p];
-    const int mod = vparams[4 * (int64_t)p + 3];
-    const uint4* src = sym + (sym_off[p] + 1 + k) * 16;
-    uint4* dst = soft + soft_off[p] / 16;
-    const uint32_t* cp = EQ ? chan + (int64_t)p * 64 : nullptr;
-    switch (mod) {
-      case 0: data_fft_symbol<0, EQ>(src, k, lut, dst + k * 3, cp, T); break;
-      case 1: data_fft_symbol<1, EQ>(src, k, lut, dst + k * 6, cp, T); break;
-      case 2: data_fft_symbol<2, EQ>(src, k, lut, dst + k * 12, cp, T); break;
-      default: data_fft_symbol<3, EQ>(src, k, lut, dst + k * 18, cp, T); break;
+    const int mod = valid ? vparams[4 * (int64_t)p + 3] : 0;
+    const uint32_t sidx = valid ? (uint32_t)(sym_off[p] + 1 + k) : 0u;                  // symbol index
+    const uint32_t nu = valid ? (uint32_t)soft_units_of(mod) : 0u;
+    const uint32_t obase = valid ? (uint32_t)(soft_off[p] / 16) + (uint32_t)k * nu : 0u;  // soft row, 16-B units
+    // ---- in: 16 x 1 KiB LDS-DMA loads, chunk c of symbol s to unit 16s + ((c + s) & 15)
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const int s = 4 * i + (lane >> 4);
+      const uint32_t si = (uint32_t)__shfl((int)sidx, s);
+      const int c = ((lane & 15) - s) & 15;
+      if (w * 64 + s < total)
+        __builtin_amdgcn_global_load_lds((const void*)(symb + (size_t)si * 256 + 16 * c),
+                                         (__attribute__((address_space(3))) void*)(stage + 64 * i), 16, 0, 0);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s2 x[64];
+#pragma unroll
+    for (int c = 0; c < 16; c++) {
+      const uint4 v = stage[16 * lane + ((c + lane) & 15)];
+      x[4 * c] = as_s2(v.x); x[4 * c + 1] = as_s2(v.y); x[4 * c + 2] = as_s2(v.z); x[4 * c + 3] = as_s2(v.w);
+    }
+    // ---- compute: every lane has read its input before any lane writes its soft row below
+    uint4* row = stage + kDfRow * lane;
+    const uint32_t* cp = EQ ? chan + (int64_t)p * 64 : nullptr;
+    if (valid) {
+      switch (mod) {
+        case 0: data_fft_symbol<0, EQ>(x, k, lut, row, cp, T); break;
+        case 1: data_fft_symbol<1, EQ>(x, k, lut, row, cp, T); break;
+        case 2: data_fft_symbol<2, EQ>(x, k, lut, row, cp, T); break;
+        default: data_fft_symbol<3, EQ>(x, k, lut, row, cp, T); break;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // ---- out: 18 x 64 units, (s, q) = divmod(64j + lane, 18)
+#pragma unroll
+    for (int j = 0; j < 18; j++) {
+      const int u = 64 * j + lane;
+      const int s = u / 18, q = u - 18 * s;
+      const uint32_t o = (uint32_t)__shfl((int)obase, s), n = (uint32_t)__shfl((int)nu, s);
+      const uint4 v = stage[kDfRow * s + q];
+      if ((uint32_t)q < n) soft[o + q] = v;
+    }
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
