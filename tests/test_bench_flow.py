@@ -119,8 +119,8 @@ def test_bench_pipelined_flow(oracle, tmp_path, args, k, w):
     assert [e[1:] for e in timed] == [[(w + i) % 2, (w + i) % nb] for i in range(k)]
     assert [e[1:] for e in verify] == [[j, bi] for bi in range(nb) for j in range(2)]
     if "--config" not in args:                      # config 3: the single-engine pass, K steps on engine 0
-        single = rest[k + 2 * nb:]
-        assert [e[1:] for e in single] == [[0, i % nb] for i in range(k)]
+        single = rest[k + 2 * nb:]                  # its own warmup, then the K timed steps
+        assert [e[1:] for e in single] == [[0, i % nb] for i in range(w)] + [[0, i % nb] for i in range(k)]
         assert line["config"]["batches_per_gpu"] == nb and b["packets"] == nb * 24
         assert line["value_one_engine"] > 0
 

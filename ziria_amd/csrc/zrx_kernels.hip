@@ -466,34 +466,91 @@ __global__ __launch_bounds__(1024) void k_pkt_rows(const int32_t* __restrict__ v
 
 // ---- k_data_fft: FFT64 + GetData + DemapLimit + Demap + Deinterleave, lane = data symbol ----
 // The FFT runs one symbol per lane (no cross-lane traffic), but a lane's 256-B symbol and its
-// 288-B soft row are a poor memory pattern: 64 rows per load or store instruction.  So each
-// wave moves its 64 symbols through its own LDS region in both directions:
-//  * in: 16 LDS-DMA loads (global_load_lds_dwordx4), each 1 KiB of 4 whole symbols.  The
-//    destination of a DMA load is lane-linear, so the skew sits on the source: LDS unit
-//    16s + ((c + s) mod 16) holds 16-B chunk c of symbol s, and lane s's 16 ds_read_b128 of
-//    chunk c land on 16 distinct 16-B slots in every lane group (conflict-free).
-//  * out: the demapper writes unit q of the soft row to 19s + q (stride 19: 8-lane groups of
-//    ds_write_b128 hit 8 slots), then 18 store instructions each take 64 consecutive units of
-//    the wave's rows (s, q) = divmod(64j + lane, 18), i.e. 1 KiB runs of consecutive rows.
+// 288-B soft row are a poor memory pattern: 64 rows per load or store instruction.  Each wave
+// can move its 64 symbols through its own LDS region (ZRX_DF_IN / ZRX_DF_OUT select, for A/B):
+//  * in (DF_IN 1, 2): 16 LDS-DMA loads (global_load_lds_dwordx4), each 1 KiB of 4 whole
+//    symbols.  The destination of a DMA load is lane-linear, so the skew sits on the source:
+//    LDS unit 16s + ((c + s) mod 16) holds 16-B chunk c of symbol s, and lane s's 16
+//    ds_read_b128 of chunk c land on 16 distinct 16-B slots in every lane group.  DF_IN 2
+//    issues the next iteration's loads as soon as this one's symbols are in registers.
+//  * out (DF_OUT 1): the demapper writes unit q of the soft row to 19s + q (stride 19: the
+//    8-lane groups of ds_write_b128 hit 8 slots), then 18 store instructions each take 64
+//    consecutive units of the wave's rows, (s, q) = divmod(64j + lane, 18): 1 KiB runs.
+// DF_IN 0 / DF_OUT 0: each lane loads / stores its own row (16 / 18 x 16 B).
 // A wave never waits on another: LDS is in order within a wave, so there are no barriers.
+#ifndef ZRX_DF_IN
+#define ZRX_DF_IN 0
+#endif
+#ifndef ZRX_DF_OUT
+#define ZRX_DF_OUT 0
+#endif
+constexpr int kDfIn = ZRX_DF_IN, kDfOut = ZRX_DF_OUT;
 constexpr int kDfWaves = 4;           // waves per block
 constexpr int kDfRow = 19;            // output staging row stride, 16-B units (a soft row is <= 18)
-constexpr int kDfStage = 64 * kDfRow; // units per wave (>= 1024 units of input)
+constexpr int kDfInUnits = kDfIn ? 1024 : 0;
+constexpr int kDfOutUnits = kDfOut ? 64 * kDfRow : 0;
+// one region per wave: input and output share it unless the input is prefetched
+constexpr int kDfUnits = kDfIn == 2 ? kDfInUnits + kDfOutUnits : (kDfInUnits > kDfOutUnits ? kDfInUnits : kDfOutUnits);
+constexpr int kDfOutBase = kDfIn == 2 ? kDfInUnits : 0;
 constexpr int kDfLutCopies = 4;       // demap LUT copies (lane & 3): fewer LDS bank conflicts
-constexpr int kDfBlocksPerCu = 2;     // 2 x 80 KiB of LDS
+constexpr int kDfLdsBytes = kDfWaves * kDfUnits * 16 + 256 * kDfLutCopies * 4;
+constexpr int kDfBlocksPerCu = kDfLdsBytes == 0 ? 4 : (160 * 1024) / kDfLdsBytes < 1 ? 1
+                             : (160 * 1024) / kDfLdsBytes > 4 ? 4 : (160 * 1024) / kDfLdsBytes;
 
-template <int MOD>
-__host__ __device__ constexpr int soft_units() { return ModInfo<MOD>::ncbps / 16; }
 __device__ __forceinline__ int soft_units_of(int mod) { return mod == 0 ? 3 : mod == 1 ? 6 : mod == 2 ? 12 : 18; }
 
-template <int MOD, bool EQ>
-__device__ __forceinline__ void data_fft_symbol(s2* x, int k, const uint32_t* lut, uint4* row,
+template <int MOD, bool EQ, class St>
+__device__ __forceinline__ void data_fft_symbol(s2* x, int k, const uint32_t* lut, St st,
                                                 const uint32_t* __restrict__ cp, const EqTabs& T) {
   fft64_inplace(x);
   if constexpr (EQ) equalize_data_bins(x, [cp](int b) { return as_s2(cp[b]); }, k + 1, T);
-  demap_deinterleave_st<MOD>(x, [lut](uint32_t i) { return lut[i * kDfLutCopies]; },
-                             [row](int q, uint4 v) { row[q] = v; });
+  demap_deinterleave_st<MOD>(x, [lut](uint32_t i) { return lut[i * kDfLutCopies]; }, st);
 }
+
+// This lane's symbol of wave w: packet, index in the packet, modulation, symbol index, soft row.
+struct DfSym {
+  bool valid;
+  int p, k, mod;
+  uint32_t sidx, nu, obase;   // obase: soft row in 16-B units
+};
+__device__ __forceinline__ DfSym df_sym(int w, int lane, int total, const int64_t* __restrict__ sym_off,
+                                        const int32_t* __restrict__ vparams, const int64_t* __restrict__ soft_off,
+                                        const int32_t* __restrict__ dsym, const int32_t* __restrict__ wave_p0) {
+  DfSym d;
+  const int g = w * 64 + lane;
+  d.valid = g < total;
+  int p = wave_p0[w];
+  if (d.valid)
+    while (dsym[p + 1] <= g) p++;                    // packets of fewer than 64 symbols
+  d.p = p;
+  d.k = g - dsym[p];
+  d.mod = d.valid ? vparams[4 * (int64_t)p + 3] : 0;
+  d.sidx = d.valid ? (uint32_t)(sym_off[p] + 1 + d.k) : 0u;
+  d.nu = d.valid ? (uint32_t)soft_units_of(d.mod) : 0u;
+  d.obase = d.valid ? (uint32_t)(soft_off[p] / 16) + (uint32_t)d.k * d.nu : 0u;
+  return d;
+}
+// 16 LDS-DMA loads of wave w's symbols into buf (1 KiB each; chunk c of symbol s at unit
+// 16s + ((c + s) & 15))
+__device__ __forceinline__ void df_load_lds(const char* symb, uint4* buf, const DfSym& d, int w, int total, int lane) {
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const int s = 4 * i + (lane >> 4);
+    const uint32_t si = (uint32_t)__shfl((int)d.sidx, s);
+    const int c = ((lane & 15) - s) & 15;
+    if (w * 64 + s < total)
+      __builtin_amdgcn_global_load_lds((const void*)(symb + (size_t)si * 256 + 16 * c),
+                                       (__attribute__((address_space(3))) void*)(buf + 64 * i), 16, 0, 0);
+  }
+}
+__device__ __forceinline__ void df_read_lds(const uint4* buf, int lane, s2* x) {
+#pragma unroll
+  for (int c = 0; c < 16; c++) {
+    const uint4 v = buf[16 * lane + ((c + lane) & 15)];
+    x[4 * c] = as_s2(v.x); x[4 * c + 1] = as_s2(v.y); x[4 * c + 2] = as_s2(v.z); x[4 * c + 3] = as_s2(v.w);
+  }
+}
+
 // Flat over the batch's data symbols (k_pkt_plan numbers them): wave w takes symbols
 // 64w .. 64w+63, lane = symbol, whatever packets they belong to, so a long packet spreads
 // over many waves and consecutive lanes write consecutive soft rows.  Waves loop over w with
@@ -504,7 +561,7 @@ __global__ __launch_bounds__(256) void k_data_fft(const uint4* __restrict__ sym,
                                                   uint4* __restrict__ soft, const int64_t* __restrict__ soft_off,
                                                   const int32_t* __restrict__ dsym, const int32_t* __restrict__ wave_p0,
                                                   const uint32_t* __restrict__ chan, EqTabs T) {
-  __shared__ uint4 stage_all[kDfWaves][kDfStage];
+  __shared__ uint4 stage_all[kDfWaves][kDfUnits > 0 ? kDfUnits : 1];
   __shared__ uint32_t lut_all[256 * kDfLutCopies];
   for (int i = threadIdx.x; i < 256 * kDfLutCopies; i += blockDim.x) lut_all[i] = kDemapLut[i / kDfLutCopies];
   __syncthreads();
@@ -515,56 +572,70 @@ __global__ __launch_bounds__(256) void k_data_fft(const uint4* __restrict__ sym,
   const char* symb = (const char*)sym;
   const int total = dsym[npkts];
   const int nw = (total + 63) >> 6;
-  for (int w = __builtin_amdgcn_readfirstlane(blockIdx.x * kDfWaves + wv); w < nw; w += gridDim.x * kDfWaves) {
-    const int g = w * 64 + lane;
-    const bool valid = g < total;
-    int p = wave_p0[w];
-    if (valid)
-      while (dsym[p + 1] <= g) p++;                  // packets of fewer than 64 symbols
-    const int k = g - dsym[p];
-    const int mod = valid ? vparams[4 * (int64_t)p + 3] : 0;
-    const uint32_t sidx = valid ? (uint32_t)(sym_off[p] + 1 + k) : 0u;                  // symbol index
-    const uint32_t nu = valid ? (uint32_t)soft_units_of(mod) : 0u;
-    const uint32_t obase = valid ? (uint32_t)(soft_off[p] / 16) + (uint32_t)k * nu : 0u;  // soft row, 16-B units
-    // ---- in: 16 x 1 KiB LDS-DMA loads, chunk c of symbol s to unit 16s + ((c + s) & 15)
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-      const int s = 4 * i + (lane >> 4);
-      const uint32_t si = (uint32_t)__shfl((int)sidx, s);
-      const int c = ((lane & 15) - s) & 15;
-      if (w * 64 + s < total)
-        __builtin_amdgcn_global_load_lds((const void*)(symb + (size_t)si * 256 + 16 * c),
-                                         (__attribute__((address_space(3))) void*)(stage + 64 * i), 16, 0, 0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int wstep = gridDim.x * kDfWaves;
+  int w = __builtin_amdgcn_readfirstlane(blockIdx.x * kDfWaves + wv);
+  DfSym d;
+  if (w < nw) {
+    d = df_sym(w, lane, total, sym_off, vparams, soft_off, dsym, wave_p0);
+    if constexpr (kDfIn == 2) df_load_lds(symb, stage, d, w, total, lane);
+  }
+  for (; w < nw; w += wstep) {
     s2 x[64];
-#pragma unroll
-    for (int c = 0; c < 16; c++) {
-      const uint4 v = stage[16 * lane + ((c + lane) & 15)];
-      x[4 * c] = as_s2(v.x); x[4 * c + 1] = as_s2(v.y); x[4 * c + 2] = as_s2(v.z); x[4 * c + 3] = as_s2(v.w);
+    if constexpr (kDfIn == 0) {
+      load_symbol(sym + (size_t)d.sidx * 16, x);
+    } else {
+      if constexpr (kDfIn == 1) df_load_lds(symb, stage, d, w, total, lane);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      df_read_lds(stage, lane, x);
     }
-    // ---- compute: every lane has read its input before any lane writes its soft row below
-    uint4* row = stage + kDfRow * lane;
-    const uint32_t* cp = EQ ? chan + (int64_t)p * 64 : nullptr;
-    if (valid) {
-      switch (mod) {
-        case 0: data_fft_symbol<0, EQ>(x, k, lut, row, cp, T); break;
-        case 1: data_fft_symbol<1, EQ>(x, k, lut, row, cp, T); break;
-        case 2: data_fft_symbol<2, EQ>(x, k, lut, row, cp, T); break;
-        default: data_fft_symbol<3, EQ>(x, k, lut, row, cp, T); break;
+    // the next iteration's symbols: located now, loaded now with DF_IN 2 (every lane has
+    // read its input above before the DMA overwrites it)
+    const int wn = w + wstep;
+    DfSym dn;
+    if (wn < nw) {
+      dn = df_sym(wn, lane, total, sym_off, vparams, soft_off, dsym, wave_p0);
+      if constexpr (kDfIn == 2) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        df_load_lds(symb, stage, dn, wn, total, lane);
       }
     }
-    __builtin_amdgcn_wave_barrier();
-    // ---- out: 18 x 64 units, (s, q) = divmod(64j + lane, 18)
-#pragma unroll
-    for (int j = 0; j < 18; j++) {
-      const int u = 64 * j + lane;
-      const int s = u / 18, q = u - 18 * s;
-      const uint32_t o = (uint32_t)__shfl((int)obase, s), n = (uint32_t)__shfl((int)nu, s);
-      const uint4 v = stage[kDfRow * s + q];
-      if ((uint32_t)q < n) soft[o + q] = v;
+    // ---- compute
+    const uint32_t* cp = EQ ? chan + (int64_t)d.p * 64 : nullptr;
+    if (d.valid) {
+      if constexpr (kDfOut == 1) {
+        uint4* row = stage + kDfOutBase + kDfRow * lane;
+        auto st = [row](int q, uint4 v) { row[q] = v; };
+        switch (d.mod) {
+          case 0: data_fft_symbol<0, EQ>(x, d.k, lut, st, cp, T); break;
+          case 1: data_fft_symbol<1, EQ>(x, d.k, lut, st, cp, T); break;
+          case 2: data_fft_symbol<2, EQ>(x, d.k, lut, st, cp, T); break;
+          default: data_fft_symbol<3, EQ>(x, d.k, lut, st, cp, T); break;
+        }
+      } else {
+        uint4* row = soft + d.obase;
+        auto st = [row](int q, uint4 v) { row[q] = v; };
+        switch (d.mod) {
+          case 0: data_fft_symbol<0, EQ>(x, d.k, lut, st, cp, T); break;
+          case 1: data_fft_symbol<1, EQ>(x, d.k, lut, st, cp, T); break;
+          case 2: data_fft_symbol<2, EQ>(x, d.k, lut, st, cp, T); break;
+          default: data_fft_symbol<3, EQ>(x, d.k, lut, st, cp, T); break;
+        }
+      }
     }
-    __builtin_amdgcn_wave_barrier();
+    if constexpr (kDfOut == 1) {
+      __builtin_amdgcn_wave_barrier();
+      // ---- out: 18 x 64 units, (s, q) = divmod(64j + lane, 18)
+#pragma unroll
+      for (int j = 0; j < 18; j++) {
+        const int u = 64 * j + lane;
+        const int s = u / 18, q = u - 18 * s;
+        const uint32_t o = (uint32_t)__shfl((int)d.obase, s), n = (uint32_t)__shfl((int)d.nu, s);
+        const uint4 v = stage[kDfOutBase + kDfRow * s + q];
+        if ((uint32_t)q < n) soft[o + q] = v;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    d = dn;
   }
 }
 
