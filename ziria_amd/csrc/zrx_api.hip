@@ -37,6 +37,7 @@ struct zrx_ctx {
   int device = 0;
   int ncu = 256;                  // compute units (k_pkt_plan: segment length, block placement)
   int crc_blocks = 1024;          // k_descramble_crc grid cap (blocks of kCrcWaves packets)
+  int df_blocks = 512, df_blocks_eq = 512;   // k_data_fft grid: the blocks resident at once (no tail round)
 #ifdef ZRX_EXPERIMENTS
   // A/B builds only (scripts/build_variant.sh): environment knobs that select other kernels
   int v3dbg = 0;                  // ZRX_V3DBG: k_viterbi3 timing-experiment variants (wrong output)
@@ -415,6 +416,13 @@ int zrx_create(zrx_ctx** out, int device, void* stream) {
   c->device = device;
   ZRX_CHECK(hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device));
   c->stream = (hipStream_t)stream;
+  // k_data_fft loops its waves over the batch: launch exactly the blocks that are resident at
+  // once (occupancy from its VGPRs and LDS), so no second round of blocks runs alone at the end
+  int occ = 0;
+  ZRX_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_data_fft<false>, 256, 0));
+  c->df_blocks = std::max(1, occ) * c->ncu;
+  ZRX_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_data_fft<true>, 256, 0));
+  c->df_blocks_eq = std::max(1, occ) * c->ncu;
 #ifdef ZRX_EXPERIMENTS
   if (const char* v = std::getenv("ZRX_VITERBI")) {
     const int k = std::atoi(v);
@@ -649,7 +657,7 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
   if (ev) ZRX_CHECK(hipEventRecord(ev[2], s));
   // k_data_fft: waves over the batch's data symbols, at most npkts x (max_nsym - 1) of them
   const int fft_blocks = (int)std::min<int64_t>(((int64_t)npkts * (max_nsym - 1) + 255) / 256,
-                                                (int64_t)kDfBlocksPerCu * c->ncu);
+                                                (int64_t)(chan ? c->df_blocks_eq : c->df_blocks));
   if (fft_blocks > 0) {
     if (chan)
       k_data_fft<true><<<fft_blocks, 256, 0, s>>>((const uint4*)d_sym, d_sym_off, c->vparams, npkts, (uint4*)c->soft,

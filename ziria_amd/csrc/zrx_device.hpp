@@ -136,17 +136,18 @@ __device__ __forceinline__ void demap_deinterleave(const s2* x, const uint32_t* 
 // demap_deinterleave that hands each group of 4 words (16 soft bytes) to st(q, uint4) as
 // soon as it is built, so the whole soft symbol never has to be live in registers.
 // lut(i) returns kDemapLut[i] (k_data_fft reads one of several LDS copies per lane).
+// Each LUT byte is a soft value 0..7, so one dword per subcarrier holds both components:
+// lut(re) in bits 0..2 of each byte, lut(im) in bits 4..6 (half the registers of two arrays).
 template <int MOD, class Lut, class St>
 __device__ __forceinline__ void demap_deinterleave_st(const s2* x, Lut lut, St st) {
   constexpr int NB = ModInfo<MOD>::nb, NC = ModInfo<MOD>::ncbps;
-  uint32_t lr[48], li[48];
+  uint32_t lri[48];
 #pragma unroll
   for (int i = 0; i < 48; i++) {
     s2 v = x[bitrev6(data_bin(i))];
     v = __builtin_elementwise_max(__builtin_elementwise_min(v, (s2){127, 127}), (s2){-128, -128});
     const uint32_t u = as_u32(v);
-    lr[i] = lut(u & 0xFF);
-    li[i] = (MOD == 0) ? 0u : lut((u >> 16) & 0xFF);
+    lri[i] = lut(u & 0xFF) | ((MOD == 0) ? 0u : lut((u >> 16) & 0xFF) << 4);
   }
 #pragma unroll
   for (int q = 0; q < NC / 16; q++) {
@@ -158,8 +159,7 @@ __device__ __forceinline__ void demap_deinterleave_st(const s2* x, Lut lut, St s
       for (int b = 0; b < 4; b++) {
         const int j = deint_src<MOD>(16 * q + 4 * e + b);
         const int i = j / NB, c = j % NB;
-        const uint32_t src = soft_comp<MOD>(c) ? li[i] : lr[i];
-        word |= ((src >> (8 * soft_lutbyte<MOD>(c))) & 0xFFu) << (8 * b);
+        word |= ((lri[i] >> (8 * soft_lutbyte<MOD>(c) + 4 * soft_comp<MOD>(c))) & 7u) << (8 * b);
       }
       w4[e] = word;
     }

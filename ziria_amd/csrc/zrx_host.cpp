@@ -195,6 +195,21 @@ __attribute__((target("avx2"))) inline void r4_v(__m256i& a, __m256i& b, __m256i
   d = mul_shift_v(_mm256_adds_epi16(a_c, jb), tw(3, 0), tw(3, 1));
 }
 
+// FFTSSEEx<4> on the 4 complex16 of each 128-bit lane (as fft4): y = x >> 2, S = (A, B, A, B)
+// with A = y0 + y2, B = y1 + y3, D = (L, T, L, T) with L = y0 + ~y2, T = y1 + ~y3; the outputs
+// A + B, ~B + A, L + ~jT, L + jT are (A, A, L, L) + (B, ~B, ~jT, jT), all saturating.
+__attribute__((target("avx2"))) inline __m256i fft4_v(__m256i v) {
+  const __m256i y = _mm256_srai_epi16(v, 2);
+  const __m256i a02 = _mm256_shuffle_epi32(y, 0x44), b13 = _mm256_shuffle_epi32(y, 0xEE);   // (y0,y1,y0,y1), (y2,y3,y2,y3)
+  const __m256i S = _mm256_adds_epi16(a02, b13);
+  const __m256i D = _mm256_adds_epi16(a02, _mm256_xor_si256(b13, _mm256_set1_epi32(-1)));
+  const __m256i J = mulj_v(D);
+  const __m256i F = _mm256_unpacklo_epi64(_mm256_shuffle_epi32(S, 0x00), _mm256_shuffle_epi32(D, 0x00));
+  const __m256i G = _mm256_xor_si256(_mm256_unpacklo_epi64(_mm256_shuffle_epi32(S, 0x55), _mm256_shuffle_epi32(J, 0x55)),
+                                     _mm256_setr_epi32(0, -1, -1, 0, 0, -1, -1, 0));
+  return _mm256_adds_epi16(F, G);
+}
+
 __attribute__((target("avx2"))) void fft64_avx2(const c16* in, c16* out) {
   static const Fft64Tables T;
   alignas(32) c16 x[64];
@@ -222,9 +237,8 @@ __attribute__((target("avx2"))) void fft64_avx2(const c16* in, c16* out) {
     v[4 * p + 2] = _mm256_permute2x128_si256(a, b, 0x31);
     v[4 * p + 3] = _mm256_permute2x128_si256(c, d, 0x31);
   }
-  for (int i = 0; i < 8; i++) _mm256_store_si256((__m256i*)(x + 8 * i), v[i]);
-  // base case FFTSSEEx<4> on the 16 groups of 4 (scalar: short dependent chains)
-  for (int g = 0; g < 16; g++) fft4(x + 4 * g);
+  // base case FFTSSEEx<4> on the 16 groups of 4: one group per 128-bit lane
+  for (int i = 0; i < 8; i++) _mm256_store_si256((__m256i*)(x + 8 * i), fft4_v(v[i]));
   // bFFT64LUTMap: natural-order bin k is x[bitrev6(k)]
   for (int k = 0; k < 64; k++) {
     const int r = ((k & 1) << 5) | ((k & 2) << 3) | ((k & 4) << 1) | ((k & 8) >> 1) | ((k & 16) >> 3) | ((k & 32) >> 5);
