@@ -144,6 +144,7 @@ extern "C" {
 #define ZRX_EHIP (-2)      /* HIP runtime error */
 #define ZRX_ENOMEM (-3)    /* workspace too small / allocation failed */
 #define ZRX_ENODEV (-4)    /* no gfx950 device */
+#define ZRX_EPLAN (-5)     /* the Viterbi plan dropped rows past its bound (zrx_plan_check) */
 
 /* packet status in pkt_info[5] */
 #define ZRX_PKT_OK 0
@@ -190,6 +191,9 @@ int zrx_viterbi_dev(zrx_ctx* ctx, const int8_t* d_soft, const int64_t* d_soft_of
  * to fill the GPU), stats2[1] = frames the seam pass re-decoded from a seam whose two
  * segments disagreed (DESIGN.md "Trellis segments"). */
 int zrx_plan_stats(zrx_ctx* ctx, int32_t* stats2);
+/* ZRX_OK, or ZRX_EPLAN if the last plan dropped rows past the bound its workspace was sized
+ * for (those packets would be left undecoded; never expected).  Synchronizes. */
+int zrx_plan_check(zrx_ctx* ctx);
 
 /* Full chain; d_sym_off: int64 symbol index of each packet's SIGNAL symbol; d_nsym: int32
  * symbols available per packet; max_nsym: the largest d_nsym, which must fit the reserved

@@ -100,6 +100,28 @@ static void stream_round_trip(int m, int plen) {
   free(out); free(x20); free(x40); free(in);
 }
 
+/* A frame longer than the 40000-column trellis (frame_len 6000): the oracle and the port's
+   batched brick stop consuming at the cap instead of reading and writing past it; both
+   produce the same windows up to there. */
+static void over_cap(void) {
+  const int fl = 6000, n = 48 * 2100;                  /* 100800 soft values, rate 1/2: 50400 columns */
+  int8_t* soft = malloc(n);
+  for (int i = 0; i < n; i++) soft[i] = (int8_t)(rnd() & 7);
+  zo_vit v; memset(&v, 0, sizeof(v));
+  CHECK(zo_vit_init(&v, fl, 0, 256) == 0, "vit_init");
+  uint8_t* a = calloc(fl + 64, 1);
+  uint8_t* b = calloc(fl + 64, 1);
+  const int got = zo_vit_decode(&v, soft, n, a);
+  CHECK(got > 0 && got < 40000 && got % 256 == 0, "over-cap frame: %d bits", got);
+  const int64_t off = 0, oo = 0;
+  const int32_t sl = n, flen = fl;
+  const int16_t cr = 0;
+  zp_viterbi_batch(soft, &off, &sl, &flen, &cr, 1, b, &oo, 1);
+  CHECK(memcmp(a, b, (size_t)got / 8) == 0, "over-cap frame: port differs from the oracle");
+  zo_vit_free(&v);
+  free(soft); free(a); free(b);
+}
+
 /* Viterbi brick: encoded random frames (zero-padded to whole 48-soft blocks, as the RX
    feeds it), fed whole, per 48-soft call and per 7 x 48 */
 static void viterbi_calls(int cr, int fl, int depth) {
@@ -244,6 +266,7 @@ int main(void) {
   for (int cr = 0; cr < 3; cr++)
     for (unsigned d = 0; d < sizeof(depths) / sizeof(depths[0]); d++) viterbi_calls(cr, 1 + 37 * cr + 100 * d, depths[d]);
   batches();
+  over_cap();
   /* corrupt SIGNAL: random bits in every header field, no packet behind it */
   for (int t = 0; t < 64; t++) {
     zo_c16 sub[48 * 4];

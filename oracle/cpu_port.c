@@ -249,6 +249,7 @@ static int pv_decode_avx512(pv_t* v, const int8_t* soft, int n, uint8_t* out) {
   const uint32_t tr_end = v->frame_len * 8 + 6;
   for (int g = 0; g + G <= n; g += G) {
     const int ns = v->cr + 1;
+    if (v->tr + (uint32_t)ns >= 40000u) break;        /* TRELLIS_MAX (sora_ext_viterbi.cpp:39): as zo_vit_decode */
     for (int st = 0; st < ns; st++) {
       int t0, t1, t2, t3;                              /* BM table by 2A+B: BM(v,e) = e ? 14-2v : 2v */
       if (st == 0) {

@@ -399,6 +399,10 @@ int zo_vit_decode(zo_vit* v, const int8_t* soft, int n, uint8_t* out) {
   uint32_t total_bytes = 0;
   uint8_t tmp[4096];
   while (in < end) {
+    /* the brick's trellis has TRELLIS_MAX = 40000 columns (sora_ext_viterbi.cpp:39) and it
+       writes past them; here (as in the engine) groups that do not fit are not consumed */
+    const uint32_t steps = v->code_rate == 0 ? 1u : v->code_rate == 1 ? 2u : 3u;
+    if (v->tr + steps >= 40000u) break;
     if (v->code_rate == 0) { step(v, in[0], in[1], 3); in += 2; }
     else if (v->code_rate == 2) { step(v, in[0], in[1], 3); step(v, in[2], 0, 1); step(v, in[3], 0, 2); in += 4; }
     else if (v->code_rate == 1) { step(v, in[0], in[1], 3); step(v, in[2], 0, 1); in += 3; }

@@ -200,6 +200,7 @@ def test_chain_mixed_distinct_large(engine, oracle):
     n = m["sym_off"].numel()
     engine.reserve(n, m["max_nsym"])
     pay, info = engine.rx(m["sym"], m["sym_off"], m["nsym"], m["max_nsym"])
+    engine.plan_check()                                   # no Viterbi row dropped past the plan's bound
     pay, info = pay.cpu().numpy(), info.cpu().numpy()
     valid = m["meta"][:, 2] <= 2048
     assert (info[valid, 4] == 1).all(), np.nonzero(valid & (info[:, 4] != 1))[0][:10]

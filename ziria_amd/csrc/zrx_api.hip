@@ -545,6 +545,19 @@ int zrx_plan_stats(zrx_ctx* c, int32_t* stats2) {
   return ZRX_OK;
 }
 
+int zrx_plan_check(zrx_ctx* c) {
+  if (!c) return ZRX_EINVAL;
+  if (!c->nrows) return ZRX_OK;
+  int32_t h[8];
+  ZRX_CHECK(hipMemcpyAsync(h, c->nrows, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  ZRX_CHECK(hipStreamSynchronize(c->stream));
+  if (h[v3::kPlanDropped] != 0) {
+    std::fprintf(stderr, "ziria_rx: the Viterbi plan dropped %d rows past its bound\n", h[v3::kPlanDropped]);
+    return ZRX_EPLAN;
+  }
+  return ZRX_OK;
+}
+
 int zrx_fft64_dev(zrx_ctx* c, const struct complex16* d_in, struct complex16* d_out, int64_t nsym) {
   if (!c || nsym < 0 || (nsym > 0 && (!d_in || !d_out))) return ZRX_EINVAL;
   if (nsym == 0) return ZRX_OK;

@@ -338,6 +338,9 @@ __device__ __forceinline__ void plan_rows_mixed(const int32_t* __restrict__ vpar
     nrows[v3::kPlanRows] = (int32_t)min(total, (uint32_t)rows_cap);
     nrows[v3::kPlanFixes] = 0;                         // counted by the seam pass
     nrows[v3::kPlanUniform] = 0;
+    // rows past the bound (plan_rows_max) are dropped: never by construction, but a wrong
+    // bound must show (zrx_plan_check) instead of leaving packets silently undecoded
+    nrows[v3::kPlanDropped] = total > (uint32_t)rows_cap ? (int32_t)(total - (uint32_t)rows_cap) : 0;
     nrows[v3::kPlanNcu] = (int32_t)ncu2;
   }
 }
@@ -436,6 +439,7 @@ __global__ __launch_bounds__(1024) void k_pkt_plan(const int32_t* __restrict__ v
       nrows[v3::kPlanRows] = (int32_t)min((uint32_t)npkts * n0, (uint32_t)rows_cap);
       nrows[v3::kPlanFixes] = 0;
       nrows[v3::kPlanUniform] = (int32_t)n0;
+      nrows[v3::kPlanDropped] = (uint32_t)npkts * n0 > (uint32_t)rows_cap ? (int32_t)((uint32_t)npkts * n0 - rows_cap) : 0;
       nrows[v3::kPlanNcu] = ncu;
     }
     return;

@@ -341,7 +341,7 @@ __host__ __device__ __forceinline__ uint32_t order_place(uint32_t pos, uint32_t 
   return ((r & 1u) ? base + m - 1u - c : b) * 16u + (pos & 15u);
 }
 // The plan header k_pkt_plan writes for k_viterbi3 (int32 words of the nrows buffer).
-enum PlanWord { kPlanRows = 0, kPlanFixes = 1, kPlanUniform = 2, kPlanNcu = 3, kPlanSegLen = 4 };   // (8 words)
+enum PlanWord { kPlanRows = 0, kPlanFixes = 1, kPlanUniform = 2, kPlanNcu = 3, kPlanSegLen = 4, kPlanDropped = 5 };   // (8 words)
 
 // start unit m_k of segment k >= 1 of nseg over a frame of E = 8 len + 6 columns (rounded
 // k E / nseg; with E / nseg >= kMinSeg the m_k are distinct and S_k + 256 + 64 <= E)

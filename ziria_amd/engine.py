@@ -63,6 +63,10 @@ class RxEngine:
         check(lib().zrx_plan_stats(self._h, st), "zrx_plan_stats")
         return int(st[0]), int(st[1])
 
+    def plan_check(self):
+        """Raises if the last Viterbi plan dropped rows past its workspace bound (ZRX_EPLAN)."""
+        check(lib().zrx_plan_check(self._h), "zrx_plan_check")
+
     # ------------------------------------------------------------------ launches
     def fft64(self, sym, out=None):
         """sym: int16 [S, 64, 2] on the device -> FFT64 of every symbol."""
