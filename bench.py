@@ -292,35 +292,61 @@ def _timed(step, steps, warmup):
 
 def bench_viterbi_only(args):
     """BASELINE config 2: 4096 frames of 1500 bytes, rate 1/2, soft = 7*bit + U[-2,2] clipped
-    to [0,7], 24048 soft values per frame (48-value groups), all resident in HBM."""
+    to [0,7], 24048 soft values per frame (48-value groups), all resident in HBM.
+    args.batches distinct batches (the steps rotate through them, so no step re-reads the
+    previous step's soft values from L2/MALL) and args.pipeline engines on their own streams
+    taking the steps in turn, as in main(); every frame of every batch is checked."""
     from oracle import oracle as O
     dev = torch.device("cuda", 0)
     n = args.npkts if args.npkts != 16384 else 4096
     fl = args.payload
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(0x5EED)
+    nb = args.batches
     nbits = 8 * fl + 6
     L = -(-nbits // 24) * 24                                  # 24 input bits per 48 soft values
-    u = torch.zeros((n, L), dtype=torch.uint8, device=dev)
-    u[:, :8 * fl] = torch.randint(0, 2, (n, 8 * fl), generator=gen, device=dev, dtype=torch.uint8)
-    coded = txgen._encode(u, 0).to(torch.int16)
-    noise = torch.randint(-2, 3, coded.shape, generator=gen, device=dev, dtype=torch.int16)
-    soft = torch.clamp(coded * 7 + noise, 0, 7).to(torch.int8).contiguous()
-    ns = soft.shape[1]
-    soft = soft.reshape(-1)
+    stride = -(-fl // 16) * 16
+    batches = []
+    for j in range(nb):
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(0x5EED + j)
+        u = torch.zeros((n, L), dtype=torch.uint8, device=dev)
+        u[:, :8 * fl] = torch.randint(0, 2, (n, 8 * fl), generator=gen, device=dev, dtype=torch.uint8)
+        coded = txgen._encode(u, 0).to(torch.int16)
+        noise = torch.randint(-2, 3, coded.shape, generator=gen, device=dev, dtype=torch.int16)
+        soft = torch.clamp(coded * 7 + noise, 0, 7).to(torch.int8).contiguous()
+        ns = soft.shape[1]
+        batches.append((soft.reshape(-1), torch.from_numpy(np.packbits(u[:, :8 * fl].cpu().numpy(), axis=1,
+                                                                       bitorder="little"))))
+        del u, coded, noise
     soft_off = torch.arange(n, dtype=torch.int64, device=dev) * ns
     params = torch.tensor([fl, 0, ns, 0], dtype=torch.int32, device=dev).repeat(n, 1).contiguous()
-    stride = -(-fl // 16) * 16
-    out = torch.zeros(n * stride, dtype=torch.uint8, device=dev)
     out_off = torch.arange(n, dtype=torch.int64, device=dev) * stride
-    out_bits = torch.zeros(n, dtype=torch.int32, device=dev)
-    eng = RxEngine(0)
-    eng.reserve(n, 1)
-    step = lambda: eng.viterbi(soft, soft_off, params, out, out_off, out_bits)
+    engs = [RxEngine(0) for _ in range(args.pipeline)]
+    streams = [torch.cuda.Stream(dev) for _ in engs]
+    outs = []
+    for e in engs:
+        e.reserve(n, 1)
+        outs.append((torch.zeros(n * stride, dtype=torch.uint8, device=dev),
+                     torch.zeros(n, dtype=torch.int32, device=dev)))
+    for st in streams:                                        # inputs come from the current stream
+        st.wait_stream(torch.cuda.current_stream(dev))
+    k = {"i": 0}
+
+    def run_on(j, bi):
+        with torch.cuda.stream(streams[j]):
+            engs[j].viterbi(batches[bi][0], soft_off, params, outs[j][0], out_off, outs[j][1])
+
+    def step():
+        run_on(k["i"] % len(engs), k["i"] % nb)
+        k["i"] += 1
     elapsed = _timed(step, args.steps, args.warmup)
-    sent = torch.from_numpy(np.packbits(u[:, :8 * fl].cpu().numpy(), axis=1, bitorder="little"))
-    got = out.reshape(n, stride)[:, :fl].cpu()
-    match = bool((got == sent).all()) and bool((out_bits == 8 * fl).all())
+    match = True
+    for bi in range(nb):                                      # every batch once more on every engine
+        for j in range(len(engs)):
+            run_on(j, bi)
+        torch.cuda.synchronize()
+        for o, ob in outs:
+            match &= bool((o.reshape(n, stride)[:, :fl].cpu() == batches[bi][1]).all()) and bool((ob == 8 * fl).all())
+    soft = batches[0][0]
     bits = n * fl * 8
     # CPU port (AVX-512 brick loop, identical to the oracle) on every allowed core, chunks of
     # the same frames for about --cpu-seconds
@@ -344,8 +370,9 @@ def bench_viterbi_only(args):
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (random bits, 802.11a encoder, soft 7*bit+U[-2,2])",
-        "config": {"workload": f"config2: {n} frames x {fl} B, R=1/2, {ns} soft values each"},
-        "bit_exact_check": {"frames_equal_sent": match},
+        "config": {"workload": f"config2: {n} frames x {fl} B, R=1/2, {ns} soft values each", "batches": nb},
+        "bit_exact_check": {"frames_equal_sent": match, "checked": f"every frame of all {nb} batches, every engine"},
+        "pipeline": f"{len(engs)} batches in flight (engines on separate streams, steps in turn)",
         "cpu_baseline": {"value": round(done * fl * 8 / cpu_dt / 1e6, 2), "unit": "Mbit/s", "cores": threads,
                          "kind": "port", "per_core": round(done * fl * 8 / cpu_dt / 1e6 / threads, 2), "host": host,
                          "sample": f"{done} frames of the same batch, {cpu_dt:.1f} s wall on {threads} threads (CPU "
@@ -484,16 +511,19 @@ def bench_capture(args):
     kat = fe["real_out"]
     kat_ok = bool(ok[0] and (pay[0, :kat.size] == kat).all())
     sample = min(64, n)
-    t0 = time.perf_counter()
-    cpu_ok = cpu_bits = 0
+    cpu_ok = 0
     match = True
-    for i in range(sample):
+    for i in range(sample):                              # parity sample: the oracle, capture by capture
         opay, r, odet, _, _ = O.rx_stream(caps[i])
         if r["ret"] == 0 and r["crc_ok"]:
             cpu_ok += 1
-            cpu_bits += (r["len"] - 4) * 8
             match &= bool((pay[i, :r["len"] - 4] == opay).all())
-    cpu_dt = time.perf_counter() - t0
+
+    def one(i):                                          # CRC-checked payload bits of capture i
+        _, r, _, _, _ = O.rx_stream(caps[i])
+        return (r["len"] - 4) * 8 if r["ret"] == 0 and r["crc_ok"] else 0
+    threads, host = host_cpus()
+    done, cpu_bits, cpu_dt = threaded_baseline(one, n, args.cpu_seconds, threads)
     print(json.dumps({
         "metric": "decoded Mbit/s, recorded 802.11a packet through the full receiver (BASELINE config 1)",
         "value": round(bits * args.steps / elapsed / 1e6, 2), "unit": "Mbit/s", "n_gpus": 1,
@@ -504,8 +534,10 @@ def bench_capture(args):
                    "captures_per_s": round(n * args.steps / elapsed, 1)},
         "bit_exact_check": {"kat_capture_matches_ground": kat_ok, "crc_pass": int(ok.sum()),
                             "oracle_sample_match": match, "oracle_sample_crc_pass": cpu_ok},
-        "cpu_baseline": {"value": round(cpu_bits / cpu_dt / 1e6, 3), "unit": "Mbit/s", "cores": 1,
-                         "kind": "port", "sample": f"first {sample} captures, {cpu_dt:.2f} s"},
+        "cpu_baseline": {"value": round(cpu_bits / cpu_dt / 1e6, 3), "unit": "Mbit/s", "cores": threads,
+                         "kind": "port", "host": host,
+                         "sample": f"{done} captures of the batch, {cpu_dt:.1f} s wall on {threads} threads "
+                                   "(scalar C oracle receiver(), one capture per call, calls in parallel)"},
     }), flush=True)
 
 
@@ -536,9 +568,9 @@ def bench_tx(args):
     elapsed = _timed(step, args.steps, args.warmup)
     out = d_out.cpu().numpy()
     sample = min(32, n)
-    t0 = time.perf_counter()
     match = all((out[i * per:(i + 1) * per] == O.tx_packet(pk[i])).all() for i in range(sample))
-    cpu_dt = time.perf_counter() - t0
+    threads, host = host_cpus()
+    done, cpu_bits, cpu_dt = threaded_baseline(lambda i: (O.tx_packet(pk[i]), L * 8)[1], n, args.cpu_seconds, threads)
     bits = n * L * 8
     print(json.dumps({
         "metric": "transmitted payload Mbit/s, 802.11a TX chain at 40 MHz (SURVEY §8f row 4)",
@@ -548,9 +580,34 @@ def bench_tx(args):
         "data": "synthetic payloads", "config": {"workload": f"tx: {n} packets x {L} B @ 54 Mbps, {per} samples each",
                                                  "gsamples_per_s": round(n * per * args.steps / elapsed / 1e9, 2)},
         "bit_exact_check": {"oracle_sample_match": bool(match), "sample": sample},
-        "cpu_baseline": {"value": round(sample * L * 8 / cpu_dt / 1e6, 2), "unit": "Mbit/s", "cores": 1,
-                         "kind": "port", "sample": f"first {sample} packets, {cpu_dt:.2f} s (oracle TX + compare)"},
+        "cpu_baseline": {"value": round(cpu_bits / cpu_dt / 1e6, 2), "unit": "Mbit/s", "cores": threads,
+                         "kind": "port", "host": host,
+                         "sample": f"{done} packets of the batch, {cpu_dt:.1f} s wall on {threads} threads "
+                                   "(scalar C oracle transmitter(), one packet per call, calls in parallel)"},
     }), flush=True)
+
+
+def threaded_baseline(fn, n, seconds, threads):
+    """Runs fn(i) for items i = 0, 1, ... (mod n) on `threads` Python threads (the oracle's
+    ctypes calls release the GIL) until `seconds` of wall time have passed; returns (items
+    done, sum of fn's results, seconds)."""
+    import concurrent.futures as cf
+    import itertools
+    done = total = 0
+    ctr = itertools.count()
+    t0 = time.perf_counter()
+
+    def worker():
+        k = s = 0
+        while time.perf_counter() - t0 < seconds or k == 0:
+            s += fn(next(ctr) % n)
+            k += 1
+        return k, s
+    with cf.ThreadPoolExecutor(max_workers=threads) as ex:
+        for k, s in ex.map(lambda _: worker(), range(threads)):
+            done += k
+            total += s
+    return done, total, time.perf_counter() - t0
 
 
 def host_cpus():

@@ -66,6 +66,16 @@ HARNESS = textwrap.dedent("""
             for i, r in enumerate(res):
                 info[i, :5] = torch.tensor([r["modulation"], r["coding"], r["len"], r["err"], r["crc_ok"]])
 
+        def viterbi(self, soft, soft_off, params, out, out_off, out_bits):
+            b = batches.setdefault(soft.data_ptr(), len(batches))
+            log.append(("vit", self.id, b))
+            n = soft_off.numel()
+            p = params.numpy()
+            o = O.viterbi_batch(soft.numpy(), soft_off.numpy(), p[:, 2], p[:, 0], p[:, 1], out_off.numpy(),
+                                out.numel(), nthreads=4, fast=True)
+            out[:] = torch.from_numpy(o)
+            out_bits[:] = torch.from_numpy(p[:, 0] * 8)
+
     bench.RxEngine = Engine
     make, mixed = txgen.make_batch_range, txgen.make_mixed_fast
     bench.txgen = types.SimpleNamespace(**{k: getattr(txgen, k) for k in dir(txgen) if not k.startswith("__")})
@@ -123,6 +133,18 @@ def test_bench_pipelined_flow(oracle, tmp_path, args, k, w):
         assert [e[1:] for e in single] == [[0, i % nb] for i in range(w)] + [[0, i % nb] for i in range(k)]
         assert line["config"]["batches_per_gpu"] == nb and b["packets"] == nb * 24
         assert line["value_one_engine"] > 0
+
+
+def test_bench_viterbi_only_flow(oracle, tmp_path):
+    """Config 2: two soft batches, two engines; the steps alternate engines and batches and
+    every frame of both batches is checked on both engines."""
+    line, logs = _run(tmp_path, ["--config", "2", "--npkts", "8", "--payload", "100", "--steps", "3",
+                                 "--warmup", "1", "--cpu-seconds", "0.2"])
+    log = [e[1:] for e in logs[0] if e[0] == "vit"]
+    assert log[:4] == [[i % 2, i % 2] for i in range(4)]
+    assert log[4:] == [[j, b] for b in range(2) for j in range(2)]
+    assert line["bit_exact_check"]["frames_equal_sent"] is True and line["config"]["batches"] == 2
+    assert line["cpu_baseline"]["value"] > 0
 
 
 def test_bench_gpus2_spawns_two_ranks(oracle, tmp_path):

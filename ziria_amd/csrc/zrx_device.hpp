@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+
 #include "zrx_tables.h"
 
 namespace zrx {
@@ -136,35 +138,55 @@ __device__ __forceinline__ void demap_deinterleave(const s2* x, const uint32_t* 
 // demap_deinterleave that hands each group of 4 words (16 soft bytes) to st(q, uint4) as
 // soon as it is built, so the whole soft symbol never has to be live in registers.
 // lut(i) returns kDemapLut[i] (k_data_fft reads one of several LDS copies per lane).
-// Each LUT byte is a soft value 0..7, so one dword per subcarrier holds both components:
-// lut(re) in bits 0..2 of each byte, lut(im) in bits 4..6 (half the registers of two arrays).
+// Each output dword takes its 4 soft bytes from 4 different subcarrier components (the
+// deinterleaver spreads neighbours), and each LUT dword holds the soft values as whole bytes,
+// so a word is two byte gathers (v_perm, the other bytes zero) and an OR.
+template <int MOD, int K>
+__host__ __device__ constexpr uint32_t soft_src(int b) {   // (register id i*2+comp) of byte b of word K
+  return (uint32_t)(2 * (deint_src<MOD>(4 * K + b) / ModInfo<MOD>::nb) + soft_comp<MOD>(deint_src<MOD>(4 * K + b) % ModInfo<MOD>::nb));
+}
+template <int MOD, int K>
+__host__ __device__ constexpr uint32_t soft_byte(int b) {  // LUT byte of byte b of word K
+  return (uint32_t)soft_lutbyte<MOD>(deint_src<MOD>(4 * K + b) % ModInfo<MOD>::nb);
+}
+// v_perm selector placing byte lo of S1 at position b0 and byte hi of S0 at position b1, zeros elsewhere
+__host__ __device__ constexpr uint32_t perm_sel2(int b0, uint32_t lo, int b1, uint32_t hi) {
+  uint32_t s = 0x0C0C0C0Cu;
+  s &= ~(0xFFu << (8 * b0)); s |= lo << (8 * b0);
+  s &= ~(0xFFu << (8 * b1)); s |= (4u + hi) << (8 * b1);
+  return s;
+}
+template <int MOD, int K>
+__device__ __forceinline__ uint32_t soft_word(const uint32_t* lr, const uint32_t* li) {
+  auto reg = [&](uint32_t id) { return (id & 1u) ? li[id >> 1] : lr[id >> 1]; };
+  const uint32_t a = __builtin_amdgcn_perm(reg(soft_src<MOD, K>(1)), reg(soft_src<MOD, K>(0)),
+                                           perm_sel2(0, soft_byte<MOD, K>(0), 1, soft_byte<MOD, K>(1)));
+  const uint32_t b = __builtin_amdgcn_perm(reg(soft_src<MOD, K>(3)), reg(soft_src<MOD, K>(2)),
+                                           perm_sel2(2, soft_byte<MOD, K>(2), 3, soft_byte<MOD, K>(3)));
+  return a | b;
+}
+template <int MOD, int Q, class St>
+__device__ __forceinline__ void soft_unit(const uint32_t* lr, const uint32_t* li, St& st) {
+  st(Q, make_uint4(soft_word<MOD, 4 * Q>(lr, li), soft_word<MOD, 4 * Q + 1>(lr, li), soft_word<MOD, 4 * Q + 2>(lr, li),
+                   soft_word<MOD, 4 * Q + 3>(lr, li)));
+}
+template <int MOD, class St, int... Q>
+__device__ __forceinline__ void soft_units(const uint32_t* lr, const uint32_t* li, St& st, std::integer_sequence<int, Q...>) {
+  (soft_unit<MOD, Q>(lr, li, st), ...);
+}
 template <int MOD, class Lut, class St>
 __device__ __forceinline__ void demap_deinterleave_st(const s2* x, Lut lut, St st) {
-  constexpr int NB = ModInfo<MOD>::nb, NC = ModInfo<MOD>::ncbps;
-  uint32_t lri[48];
+  constexpr int NC = ModInfo<MOD>::ncbps;
+  uint32_t lr[48], li[48];
 #pragma unroll
   for (int i = 0; i < 48; i++) {
     s2 v = x[bitrev6(data_bin(i))];
     v = __builtin_elementwise_max(__builtin_elementwise_min(v, (s2){127, 127}), (s2){-128, -128});
     const uint32_t u = as_u32(v);
-    lri[i] = lut(u & 0xFF) | ((MOD == 0) ? 0u : lut((u >> 16) & 0xFF) << 4);
+    lr[i] = lut(u & 0xFF);
+    li[i] = (MOD == 0) ? 0u : lut((u >> 16) & 0xFF);
   }
-#pragma unroll
-  for (int q = 0; q < NC / 16; q++) {
-    uint32_t w4[4];
-#pragma unroll
-    for (int e = 0; e < 4; e++) {
-      uint32_t word = 0;
-#pragma unroll
-      for (int b = 0; b < 4; b++) {
-        const int j = deint_src<MOD>(16 * q + 4 * e + b);
-        const int i = j / NB, c = j % NB;
-        word |= ((lri[i] >> (8 * soft_lutbyte<MOD>(c) + 4 * soft_comp<MOD>(c))) & 7u) << (8 * b);
-      }
-      w4[e] = word;
-    }
-    st(q, make_uint4(w4[0], w4[1], w4[2], w4[3]));
-  }
+  soft_units<MOD>(lr, li, st, std::make_integer_sequence<int, NC / 16>{});
 }
 
 // ------------------------------------------------------------------ ChannelEqualization + PilotTrack

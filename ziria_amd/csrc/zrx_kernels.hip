@@ -486,13 +486,11 @@ __global__ __launch_bounds__(1024) void k_pkt_rows(const int32_t* __restrict__ v
 #define ZRX_DF_IN 0
 #endif
 #ifndef ZRX_DF_OUT
-#define ZRX_DF_OUT 0
+#define ZRX_DF_OUT 1
 #endif
 constexpr int kDfIn = ZRX_DF_IN, kDfOut = ZRX_DF_OUT;
 constexpr int kDfWaves = 4;           // waves per block
-// output staging row stride, 16-B units: a whole soft row (<= 18 units, DF_OUT 1) or half of
-// one (9 units, DF_OUT 2: units 9..17 wait in registers while units 0..8 are flushed)
-constexpr int kDfRow = kDfOut == 2 ? 10 : 19;
+constexpr int kDfRow = 19;            // output staging row stride, 16-B units (a soft row is <= 18)
 constexpr int kDfInUnits = kDfIn ? 1024 : 0;
 constexpr int kDfOutUnits = kDfOut ? 64 * kDfRow : 0;
 // one region per wave: input and output share it unless the input is prefetched
@@ -561,9 +559,8 @@ __device__ __forceinline__ void df_read_lds(const uint4* buf, int lane, s2* x) {
 // 64w .. 64w+63, lane = symbol, whatever packets they belong to, so a long packet spreads
 // over many waves and consecutive lanes write consecutive soft rows.  Waves loop over w with
 // the grid's stride (the host sizes the grid from the call's max_nsym, an upper bound).
-constexpr int kDfMinWaves = kDfOut == 2 ? 3 : 1;   // half-row staging fits 3 blocks of LDS per CU
 template <bool EQ>
-__global__ __launch_bounds__(256, kDfMinWaves) void k_data_fft(const uint4* __restrict__ sym, const int64_t* __restrict__ sym_off,
+__global__ __launch_bounds__(256) void k_data_fft(const uint4* __restrict__ sym, const int64_t* __restrict__ sym_off,
                                                   const int32_t* __restrict__ vparams, int npkts,
                                                   uint4* __restrict__ soft, const int64_t* __restrict__ soft_off,
                                                   const int32_t* __restrict__ dsym, const int32_t* __restrict__ wave_p0,
@@ -608,21 +605,8 @@ __global__ __launch_bounds__(256, kDfMinWaves) void k_data_fft(const uint4* __re
     }
     // ---- compute
     const uint32_t* cp = EQ ? chan + (int64_t)d.p * 64 : nullptr;
-    uint4 hold[9];                                     // DF_OUT 2: units 9..17 of the soft row
     if (d.valid) {
-      if constexpr (kDfOut == 2) {
-        uint4* row = stage + kDfOutBase + kDfRow * lane;
-        auto st = [row, &hold](int q, uint4 v) {
-          if (q < 9) row[q] = v;
-          else hold[q - 9] = v;
-        };
-        switch (d.mod) {
-          case 0: data_fft_symbol<0, EQ>(x, d.k, lut, st, cp, T); break;
-          case 1: data_fft_symbol<1, EQ>(x, d.k, lut, st, cp, T); break;
-          case 2: data_fft_symbol<2, EQ>(x, d.k, lut, st, cp, T); break;
-          default: data_fft_symbol<3, EQ>(x, d.k, lut, st, cp, T); break;
-        }
-      } else if constexpr (kDfOut == 1) {
+      if constexpr (kDfOut == 1) {
         uint4* row = stage + kDfOutBase + kDfRow * lane;
         auto st = [row](int q, uint4 v) { row[q] = v; };
         switch (d.mod) {
@@ -652,27 +636,6 @@ __global__ __launch_bounds__(256, kDfMinWaves) void k_data_fft(const uint4* __re
         const uint32_t o = (uint32_t)__shfl((int)d.obase, s), n = (uint32_t)__shfl((int)d.nu, s);
         const uint4 v = stage[kDfOutBase + kDfRow * s + q];
         if ((uint32_t)q < n) soft[o + q] = v;
-      }
-      __builtin_amdgcn_wave_barrier();
-    } else if constexpr (kDfOut == 2) {
-      // ---- out in two halves: 9 x 64 units each, (s, q) = divmod(64j + lane, 9)
-#pragma unroll
-      for (int h = 0; h < 2; h++) {
-        if (h == 1) {
-          __builtin_amdgcn_wave_barrier();
-#pragma unroll
-          for (int q = 0; q < 9; q++)
-            if ((uint32_t)(9 + q) < d.nu) stage[kDfOutBase + kDfRow * lane + q] = hold[q];
-        }
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int j = 0; j < 9; j++) {
-          const int u = 64 * j + lane;
-          const int s = u / 9, q = u - 9 * s;
-          const uint32_t o = (uint32_t)__shfl((int)d.obase, s), n = (uint32_t)__shfl((int)d.nu, s);
-          const uint4 v = stage[kDfOutBase + kDfRow * s + q];
-          if ((uint32_t)(9 * h + q) < n) soft[o + 9 * h + q] = v;
-        }
       }
       __builtin_amdgcn_wave_barrier();
     }
