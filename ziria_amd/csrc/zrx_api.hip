@@ -545,6 +545,13 @@ int zrx_plan_stats(zrx_ctx* c, int32_t* stats2) {
   return ZRX_OK;
 }
 
+#ifdef ZRX_VTRACE
+int zrx_vtrace_set(void* p) {   // (timeline probe builds only) per-row trace buffer, 32 B per row slot
+  ZRX_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_vtrace), &p, sizeof(p)));
+  return ZRX_OK;
+}
+#endif
+
 int zrx_plan_check(zrx_ctx* c) {
   if (!c) return ZRX_EINVAL;
   if (!c->nrows) return ZRX_OK;

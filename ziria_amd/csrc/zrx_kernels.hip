@@ -629,9 +629,13 @@ __global__ __launch_bounds__(256) void k_data_fft(const uint4* __restrict__ sym,
     if constexpr (kDfOut == 1) {
       __builtin_amdgcn_wave_barrier();
       // ---- out: 18 x 64 units, (s, q) = divmod(64j + lane, 18)
+      // (lane0 is lane through an opaque move: the divmods are recomputed here each time
+      // instead of being hoisted out of the loop as 54 live registers)
+      int lane0;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(lane0) : "v"(lane));
 #pragma unroll
       for (int j = 0; j < 18; j++) {
-        const int u = 64 * j + lane;
+        const int u = 64 * j + lane0;
         const int s = u / 18, q = u - 18 * s;
         const uint32_t o = (uint32_t)__shfl((int)d.obase, s), n = (uint32_t)__shfl((int)d.nu, s);
         const uint4 v = stage[kDfOutBase + kDfRow * s + q];

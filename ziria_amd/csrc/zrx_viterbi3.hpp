@@ -874,6 +874,11 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
 //   fix:   the seam pass after a planned launch: slot = packet (segs[p] = its nseg); a row
 //          re-decodes from the first seam whose two dumps disagree (usually none).
 // The grid may be smaller than the rows (block-stride loop).
+#ifdef ZRX_VTRACE
+// (timeline probe builds only: scripts/exp/vit_trace.py) 8 words per row slot: start and end
+// (s_memrealtime, 100 MHz, low words), HW_ID, XCC_ID, block, columns, rate, packet
+__device__ uint32_t* g_vtrace;
+#endif
 template <int DBG, bool FIX>
 __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, uint32_t ncu, uint32_t ncu_rcp,
                                              const v3::Consts& K, uint8_t* ring, v3::RowX* rowx,
@@ -886,6 +891,9 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t l = lane & 15u;
   const uint32_t rib = threadIdx.x >> 4;               // row in block
+#ifdef ZRX_VTRACE
+  const uint32_t vt0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
   {
     const int slot = g0 + (int)rib;
     const bool valid = slot < nrows;
@@ -1021,6 +1029,16 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
       const bool last = (x.kn >> 16) & 1u ? work && ((x.kn >> 17) & 1u) == 0u : xk + 1u == xn;
       if (last) out_bits[x.p] = nbytes == 0xFFFFFFFFu ? -1 : (int32_t)((nbytes + (x.S >> 3)) * 8u);
     }
+#ifdef ZRX_VTRACE
+    if (!FIX && valid && l == 0 && g_vtrace) {
+      uint32_t* r = g_vtrace + 8 * (size_t)slot;
+      r[0] = vt0;
+      r[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+      r[2] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+      r[3] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+      r[4] = blockIdx.x; r[5] = colsS; r[6] = (uint32_t)cr; r[7] = (uint32_t)p;
+    }
+#endif
   }
 }
 template <int DBG, bool FIX = false>
