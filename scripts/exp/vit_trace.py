@@ -3,6 +3,7 @@ timeline of one config-5 batch and one config-3 batch.  Every row records its wa
 and end (s_memrealtime, 100 MHz), HW_ID / XCC_ID, block, columns and rate; saved to
 gpurun_out/vtrace_<cfg>.npz with a per-SIMD summary printed: when each SIMD went idle,
 how many waves it ran, how the rows' columns spread over the SIMDs."""
+import ctypes
 import os
 import sys
 
@@ -17,6 +18,9 @@ from ziria_amd.engine import RxEngine  # noqa: E402
 
 dev = torch.device("cuda", 0)
 eng = RxEngine(0)
+vtrace_set = lib().zrx_vtrace_set
+vtrace_set.argtypes = [ctypes.c_void_p, ctypes.c_int]   # (a 64-bit device pointer, not a C int)
+vtrace_set.restype = ctypes.c_int
 os.makedirs("gpurun_out", exist_ok=True)
 
 
@@ -30,10 +34,10 @@ def trace(name, b):
         eng.rx(b["sym"], b["sym_off"], b["nsym"], S, pay, info)
     torch.cuda.synchronize()
     buf = torch.zeros(65536 * 8, dtype=torch.int32, device=dev)
-    lib().zrx_vtrace_set(buf.data_ptr())
+    assert vtrace_set(buf.data_ptr(), 65536) == 0
     eng.rx(b["sym"], b["sym_off"], b["nsym"], S, pay, info)
     torch.cuda.synchronize()
-    lib().zrx_vtrace_set(0)
+    assert vtrace_set(None, 0) == 0
     rows, fixes = eng.plan_stats()
     t = buf.view(-1, 8)[:rows].cpu().numpy().astype(np.int64)
     np.savez_compressed(f"gpurun_out/vtrace_{name}.npz", t=t, rows=rows, fixes=fixes)

@@ -546,7 +546,9 @@ int zrx_plan_stats(zrx_ctx* c, int32_t* stats2) {
 }
 
 #ifdef ZRX_VTRACE
-int zrx_vtrace_set(void* p) {   // (timeline probe builds only) per-row trace buffer, 32 B per row slot
+int zrx_vtrace_set(void* p, int rows) {   // (timeline probe builds only) per-row trace buffer, 32 B per row slot
+  const uint32_t n = p ? (uint32_t)std::max(rows, 0) : 0u;
+  ZRX_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_vtrace_rows), &n, sizeof(n)));
   ZRX_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_vtrace), &p, sizeof(p)));
   return ZRX_OK;
 }

@@ -878,6 +878,7 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
 // (timeline probe builds only: scripts/exp/vit_trace.py) 8 words per row slot: start and end
 // (s_memrealtime, 100 MHz, low words), HW_ID, XCC_ID, block, columns, rate, packet
 __device__ uint32_t* g_vtrace;
+__device__ uint32_t g_vtrace_rows;                     // row slots the buffer holds
 #endif
 template <int DBG, bool FIX>
 __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, uint32_t ncu, uint32_t ncu_rcp,
@@ -1030,7 +1031,7 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
       if (last) out_bits[x.p] = nbytes == 0xFFFFFFFFu ? -1 : (int32_t)((nbytes + (x.S >> 3)) * 8u);
     }
 #ifdef ZRX_VTRACE
-    if (!FIX && valid && l == 0 && g_vtrace) {
+    if (!FIX && valid && l == 0 && g_vtrace && (uint32_t)slot < g_vtrace_rows) {
       uint32_t* r = g_vtrace + 8 * (size_t)slot;
       r[0] = vt0;
       r[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
