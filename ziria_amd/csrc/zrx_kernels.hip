@@ -304,7 +304,7 @@ __device__ __forceinline__ void plan_rows_mixed(const int32_t* __restrict__ vpar
   // Expand: the segments of the packet at sorted position i are rows prefix(i) .. +nseg - 1
   // (consecutive, so a wave holds segments of one or two packets of similar length), placed
   // snake over the CUs.  Thread t takes positions 16t .. 16t + 15 of each round.
-  const uint32_t total = *rtotal, nfull = total >> 4;
+  const uint32_t total = *rtotal, nfull = total / (uint32_t)v3::kRows;
   const uint32_t ncu2 = (uint32_t)max(ncu, 2), ncu_rcp = 0xFFFFFFFFu / ncu2 + 1u;
   __shared__ uint32_t esum[16];
   uint32_t carry = 0;

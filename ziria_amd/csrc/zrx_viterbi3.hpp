@@ -1,31 +1,37 @@
-// Batched Viterbi brick, v3: four packets per wave, 64 trellis positions per packet packed
-// as 16 lanes x 2 dwords x 2 16-bit halves.
+// Batched Viterbi brick, v3: several packets per wave, the 64 trellis positions of a packet
+// packed as kLanes lanes x kDw dwords x 2 16-bit halves (one "row" of kLanes lanes).
 //
 // Same results as the brick driver loop (csrc/sora_ext_viterbi.cpp:66-153 over
-// csrc/viterbicore.hpp:105-239) bit for bit; tests/vit3_model.py restates this layout in
-// numpy and is checked against the oracle on the CPU.
+// csrc/viterbicore.hpp:105-239) bit for bit; tests/vit3_model.py (16-lane rows) and
+// tests/vit8_model.py (8-lane rows, the default) restate the layout in numpy and are checked
+// against the reference frames and the oracle on the CPU.
 //
 //  * Labels rotate, positions stay: after t columns position p holds state rotl6(p, t mod 6),
 //    so one column maps every position's state j to rotl6(j) in place and the butterfly
-//    partner (state j ^ 32) sits at position p ^ (1 << (5 - t mod 6)).  Position bits 0/1 are
-//    the half/dword inside the lane (partners in registers); bits 2..5 are lane bits mapped
-//    to lane xor 1, 2, 15, 8 so each cross-lane partner is ONE DPP move inside the 16-lane
-//    row (quad_perm, quad_perm, row_mirror, row_ror:8).
+//    partner (state j ^ 32) sits at position p ^ (1 << (5 - t mod 6)).  Position bit 0 is the
+//    half, the next log2(kDw) bits the dword inside the lane (partners in registers), the
+//    rest lane bits: 8-lane rows map position bits 3, 4, 5 to lane xor 1, 2, 7 (DPP
+//    quad_perm, quad_perm, row_half_mirror), 16-lane rows bits 2..5 to lane xor 1, 2, 15, 8
+//    (quad_perm, quad_perm, row_mirror, row_ror:8), so each cross-lane partner is ONE DPP
+//    move inside the row.
 //  * Half = [H][pad]: H = the reference's u8 metric with its marker bit cleared (always
-//    even, wraps mod 256 in v_pk_add_u16), pad bit 7 = the marker = branch index of the
-//    source state, pad bits 6..0 = the previous decisions along the survivor path.  The
+//    even), the pad holds the decisions of the current 8-column cycle (column5).  The
 //    candidates of one column always differ in the marker, so v_pk_min_u16 reproduces
 //    min_epu8 on (metric | marker) exactly and drags the path history along with the
-//    winner (register exchange at no extra cost).  The history is shifted by one bit per
-//    column (v_lshrrev + v_bfi), and every 8 columns the pads are stored to an LDS ring
-//    indexed by state: one byte there = 8 decoded bits, so the reference traceback
+//    winner (register exchange at no extra cost).  Every 8 columns the pads are stored to an
+//    LDS ring indexed by state: one byte there = 8 decoded bits, so the reference traceback
 //    (argmin of the signed (m<<8)|4s key, `lookahead` skipped columns, bytes from the end)
 //    becomes an argmin plus one dependent LDS read per output byte.
 //  * Branch metrics: a per-column pattern word P = [BM(A=0,B=0), BM(0,1), BM(1,0), BM(1,1)]
 //    (implicit depuncturing: A-only / B-only columns have their own P, :93-110) is built
-//    once per 24-column body by lanes 0..15 of each row and broadcast with ds_swizzle;
-//    each dword gets its own branch metric with one v_perm (per-lane selector) and its
-//    complement with one v_sub from a per-lane constant.
+//    once per 24-column body by the row's lanes and broadcast with ds_swizzle; a dword gets
+//    its branch metrics with one v_perm (per-lane selector) — or shares another dword's when
+//    the state bits its dword bits flip at this phase change no expected bit (bx_src) — and
+//    its complement with one v_sub from a literal.
+//  * Why 8-lane rows: the cost per row of everything outside the column (P broadcast, walk,
+//    argmin, events) halves, one more partner phase is an in-register dword swap instead of
+//    a DPP add, and more dwords share branch-metric words (14 v_perm per 6 columns for 8
+//    states a lane instead of 10 for 4).  The LDS ring holds 16 rows per SIMD either way.
 #pragma once
 #include <utility>
 
@@ -34,9 +40,20 @@
 namespace zrx {
 namespace v3 {
 
+#ifndef ZRX_VLANES
+#define ZRX_VLANES 8
+#endif
+constexpr int kLanes = ZRX_VLANES;                     // lanes per row (packet): 8 or 16
+static_assert(kLanes == 8 || kLanes == 16, "rows are 8 or 16 lanes");
+constexpr int kDw = 32 / kLanes;                       // dwords per lane: 4 or 2
+constexpr int kDwBits = kLanes == 8 ? 2 : 1;           // position bits 1..kDwBits = the dword
+constexpr int kLaneBits = kLanes == 8 ? 3 : 4;
+constexpr int kRowsWave = 64 / kLanes;                 // rows per wave
+constexpr uint32_t kRowMask = (1u << kLanes) - 1u;     // a row's lanes in a ballot (shifted)
 constexpr int kRing = 39;                 // snapshot slots of 8 columns per packet (>= 38)
-constexpr int kRows = 16;                 // packets per 256-thread block
+constexpr int kRows = 4 * kRowsWave;      // packets per 256-thread block
 constexpr int kSlotBytes = kRows * 64;
+constexpr int kWavesPerSimd = kLanes == 8 ? 2 : 4;     // LDS ring: 16 rows per SIMD
 constexpr uint32_t kNever = 0x7FFFFFFFu;
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -51,11 +68,47 @@ __host__ __device__ constexpr uint32_t rotl6(uint32_t x, uint32_t k) {
 __host__ __device__ constexpr uint32_t rev6(uint32_t x) {
   return ((x & 1u) << 5) | ((x & 2u) << 3) | ((x & 4u) << 1) | ((x & 8u) >> 1) | ((x & 16u) >> 3) | ((x & 32u) >> 5);
 }
-// position held by (lane-in-row l, dword d, half h): lane = b2*1 ^ b3*2 ^ b4*15 ^ b5*8
-__device__ __forceinline__ uint32_t pos_of(uint32_t l, uint32_t d, uint32_t h) {
+// position held by (lane-in-row l, dword d, half h)
+//   8 lanes:  lane = b3*1 ^ b4*2 ^ b5*7        16 lanes: lane = b2*1 ^ b3*2 ^ b4*15 ^ b5*8
+__host__ __device__ constexpr uint32_t pos_of(uint32_t l, uint32_t d, uint32_t h) {
+  if (kLanes == 8) {
+    const uint32_t b5 = (l >> 2) & 1u;
+    const uint32_t b3 = (l & 1u) ^ b5, b4 = ((l >> 1) & 1u) ^ b5;
+    return h | (d << 1) | (b3 << 3) | (b4 << 4) | (b5 << 5);
+  }
   const uint32_t b4 = (l >> 2) & 1u;
   const uint32_t b2 = (l & 1u) ^ b4, b3 = ((l >> 1) & 1u) ^ b4, b5 = ((l >> 3) & 1u) ^ b4;
   return h | (d << 1) | (b2 << 2) | (b3 << 3) | (b4 << 4) | (b5 << 5);
+}
+// DPP control of the cross-lane partner for position bit pb (> kDwBits)
+__host__ __device__ constexpr int partner_dpp(int pb) {
+  return kLanes == 8 ? (pb == 5 ? 0x141 : pb == 4 ? 0x4E : 0xB1)
+                     : (pb == 5 ? 0x128 : pb == 4 ? 0x140 : pb == 3 ? 0x4E : 0xB1);
+}
+// Branch-metric word sharing (tests/vit8_model.py bx_source): the state bits dword d's
+// position bits flip at phase ph; flipping state bit 3 changes neither expected bit, bit 5
+// only the marker, bits 1 and 2 both A and B, bit 0 B, bit 4 A (encoding.blk:92-109).
+// Returns -1 (own v_perm) or e | mk << 8: dword e's word, marker bits flipped when mk.
+__host__ __device__ constexpr uint32_t dw_flips(int ph, int d) {
+  uint32_t f = 0;
+  for (int b = 0; b < kDwBits; b++)
+    if ((d >> b) & 1) f ^= 1u << ((b + 1 + ph) % 6);
+  return f;
+}
+__host__ __device__ constexpr int ab_flips(uint32_t f) {
+  int a = 0, b = 0;
+  for (int i = 0; i < 6; i++)
+    if ((f >> i) & 1) { a ^= (i == 1 || i == 2 || i == 4); b ^= (i <= 2); }
+  return 2 * a + b;
+}
+__host__ __device__ constexpr int bx_src(int ph, int d) {
+  if (d == 0) return -1;
+  const uint32_t f = dw_flips(ph, d);
+  for (int e = 0; e < d; e++) {
+    const uint32_t fe = dw_flips(ph, e);
+    if (ab_flips(f) == ab_flips(fe)) return e | (int)((((f ^ fe) >> 5) & 1u) << 8);
+  }
+  return -1;
 }
 
 // LDS byte address of a pointer into a __shared__ array (for inline-asm DS instructions)
@@ -63,22 +116,19 @@ __device__ __forceinline__ uint32_t lds_addr(const uint8_t* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)p;
 }
 
-// Per-lane constants (registers for the whole kernel).
+// Per-lane constants (registers for the whole kernel; entries no column reads are dropped).
 struct Consts {
-  uint32_t sel[6][2];     // v_perm selector: [BM_hi][bm_hi<<7][BM_lo][bm_lo<<7]
-  uint32_t sel7[3][2];    // KPH 7 columns (phases 1, 3, 5): [BM_hi + bm_hi][0][BM_lo + bm_lo][0]
-  uint32_t cf[6][2];      // per half (28 + bm) << 8: BY = cf - BX for a full column
-  uint32_t cs[6][2];      // per half (14 + bm) << 8: punctured column
-  uint32_t sa[3][4];      // LDS ring byte offset of the state held by position q at C mod 6 = 0,2,4
-  uint32_t sa2w;          // C mod 6 = 4: the 4 states of the lane are the ring dword at this offset
+  uint32_t sel[6][kDw];   // v_perm selector: [BM_hi][bm_hi<<7][BM_lo][bm_lo<<7]
+  uint32_t sel7[3][kDw];  // KPH 7 columns (phases 1, 3, 5): [BM_hi + bm_hi][0][BM_lo + bm_lo][0]
+  uint32_t sa[3];         // LDS ring byte offset of the lane's first position (dword 0, half 0) at C mod 6 = 0,2,4
 };
 
 __device__ __forceinline__ void make_consts(Consts& K, uint32_t l, uint32_t rib) {
 #pragma unroll
   for (int ph = 0; ph < 6; ph++) {
 #pragma unroll
-    for (int d = 0; d < 2; d++) {
-      uint32_t s = 0, s7 = 0, cf = 0, cs = 0;
+    for (int d = 0; d < kDw; d++) {
+      uint32_t s = 0, s7 = 0;
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         const uint32_t j = rotl6(pos_of(l, d, h), ph);
@@ -90,173 +140,110 @@ __device__ __forceinline__ void make_consts(Consts& K, uint32_t l, uint32_t rib)
         // KPH 7: byte 2A+B of P (src1) or of P | 0x01010101 (src0: BM + 1, BM even), low byte 0
         s7 |= 12u << (16 * h);
         s7 |= (2u * A + B + (bm ? 4u : 0u)) << (16 * h + 8);
-        cf |= (28u + bm) << (16 * h + 8);
-        cs |= (14u + bm) << (16 * h + 8);
       }
-      K.sel[ph][d] = s; K.cf[ph][d] = cf; K.cs[ph][d] = cs;
+      K.sel[ph][d] = s;
       if (ph & 1) K.sel7[ph >> 1][d] = s7;
     }
   }
+  // (the lane's other positions are at lane-uniform offsets from these: snap_delta)
 #pragma unroll
-  for (int k = 0; k < 3; k++)
-#pragma unroll
-    for (int q = 0; q < 4; q++) K.sa[k][q] = rib * 64u + rev6(rotl6(pos_of(l, q >> 1, q & 1), 2 * k));
-  // (column snapshots use sa[k][0] and the lane-uniform deltas of sa[k][1..3]; tests/vit3_model.py)
-  K.sa2w = K.sa[2][0] & ~3u;   // k = 2: dword address of the lane's 4 consecutive bytes (column5)
+  for (int k = 0; k < 3; k++) K.sa[k] = rib * 64u + rev6(rotl6(pos_of(l, 0, 0), 2 * k));
+}
+// ring-index offset of the position with in-lane bits (d, h) from the lane's first, at
+// snapshot k (C mod 6 = 2k): position bit b -> state bit (b + 2k) mod 6 -> ring bit 5 - that
+__host__ __device__ constexpr uint32_t snap_delta(int k, int d, int h) {
+  const uint32_t p = (uint32_t)h | ((uint32_t)d << 1);
+  uint32_t o = 0;
+  for (int b = 0; b <= kDwBits; b++)
+    if ((p >> b) & 1u) o |= 1u << (5 - (b + 2 * k) % 6);
+  return o;
 }
 
-// One trellis column (phase PH = column index mod 6 before the step), KIND 0: (a, b) on
-// (A, B); 1: a on A only; 2: a on B only.
-template <int PH, int KIND>
-__device__ __forceinline__ void column(uint32_t& M0, uint32_t& M1, uint32_t P, const Consts& K) {
-  const uint32_t T0 = ((M0 >> 1) & 0x00FF00FFu) | (M0 & 0xFF00FF00u);
-  const uint32_t T1 = ((M1 >> 1) & 0x00FF00FFu) | (M1 & 0xFF00FF00u);
-  const uint32_t BX0 = __builtin_amdgcn_perm(0x80808080u, P, K.sel[PH][0]);
-  const uint32_t BX1 = __builtin_amdgcn_perm(0x80808080u, P, K.sel[PH][1]);
-  const uint32_t BY0 = (KIND == 0 ? K.cf[PH][0] : K.cs[PH][0]) - BX0;
-  const uint32_t BY1 = (KIND == 0 ? K.cf[PH][1] : K.cs[PH][1]) - BX1;
-  const u16x2 X0 = h2(T0) + h2(BX0), X1 = h2(T1) + h2(BX1);
-  const u16x2 Y0 = h2(T0) + h2(BY0), Y1 = h2(T1) + h2(BY1);
-  if constexpr (PH <= 3) {
-    constexpr int ctrl = PH == 0 ? 0x128 : PH == 1 ? 0x140 : PH == 2 ? 0x4E : 0xB1;  // xor 8, 15, 2, 1
-    const uint32_t Z0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)w32(Y0), ctrl, 0xF, 0xF, true);
-    const uint32_t Z1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)w32(Y1), ctrl, 0xF, 0xF, true);
-    M0 = w32(__builtin_elementwise_min(X0, h2(Z0)));
-    M1 = w32(__builtin_elementwise_min(X1, h2(Z1)));
-  } else if constexpr (PH == 4) {
-    M0 = w32(__builtin_elementwise_min(X0, Y1));
-    M1 = w32(__builtin_elementwise_min(X1, Y0));
+// Shift-free column (tests/vit3_model.py Packet.step5, vit8_model.py).  The column with
+// cycle phase KPH = (c + 1) mod 8 (c = the column computed; KPH 7 is the snapshot column)
+// writes its marker at bit KPH + 1 of each half: a half is [H >> 1 in bits 15..9][the cycle's
+// decisions in bits 8..1, oldest lowest][bit 0: carry guard].  Bits above the marker are
+// still 0 in both candidates (cleared at KPH 0), so the marker breaks ties exactly like the
+// brick's metric LSB (viterbicore.hpp:105-147), and the pads need no shift: one AND per
+// dword clears the guard bit 16 that a 32-bit add carries into when H0 wraps (at KPH 0 it
+// also clears the cycle's history).  At KPH 7 the marker is bit 8, the LSB of the (even) H
+// byte: BX = [BM][bm << 7] plus its own low byte = [BM + bm][0].
+template <int PH, int KPH, int D>
+__device__ __forceinline__ void column_bx(uint32_t (&BX)[kDw], uint32_t (&BY)[kDw], uint32_t P, const Consts& K,
+                                          uint32_t C) {
+  constexpr uint32_t mk = 2u << KPH;
+  constexpr uint32_t mbits = KPH == 7 ? 0x01000100u : mk * 0x00010001u;
+  constexpr int src = bx_src(PH, D);
+  if constexpr (src < 0) {
+    if constexpr (KPH == 7) {      // [BM + bm][0] per half: BM (even) or BM + 1 = byte of P | 0x01010101
+      static_assert(PH & 1, "KPH 7 columns have odd phases (body columns 5, 13, 21)");
+      BX[D] = __builtin_amdgcn_perm(P | 0x01010101u, P, K.sel7[PH >> 1][D]);
+    } else {
+      BX[D] = __builtin_amdgcn_perm((mk & 0xFFu) * 0x01010101u, P, K.sel[PH][D]);
+    }
+  } else if constexpr ((src >> 8) == 0) {
+    BX[D] = BX[src & 0xFF];
+    BY[D] = BY[src & 0xFF];
+    return;
   } else {
-    M0 = w32(__builtin_elementwise_min(X0, Y0.yx));
-    M1 = w32(__builtin_elementwise_min(X1, Y1.yx));
+    BX[D] = BX[src & 0xFF] ^ mbits;
   }
+  // Keep C - BX a value of its own: reassociated as (partner T - BX) + C it would put two
+  // adds after the AND on the column-to-column dependency chain instead of one.
+  BY[D] = C - BX[D];
+  asm("" : "+v"(BY[D]));
 }
-
-// The same column with 32-bit adds (tests/vit3_model.py Packet.step4).  The cross candidate
-// is the partner's shifted metric plus this position's complement metric C - BX: the
-// partner state j ^ 32 has the same expected bits (A, B depend on j bits 0..4) and the
-// other marker, so C = (k << 8) | 0x80 per half is one lane-uniform literal and the partner
-// lane's T is read straight by v_add_u32_dpp (no v_mov_dpp, no v_pk_add_u16).  A 32-bit
-// add carries out of half 0 into bit 0 of half 1's pad when H0 + BM wraps; MODE keeps that
-// bit 0 at every such add: MODE 1 (the column after a snapshot) clears the pads instead of
-// shifting them, so the oldest history bit reaching bit 0 is the one already stored, and
-// MODE 2 (the snapshot column, where bit 0 is a live decision) adds exactly with
-// v_pk_add_u16.  A set bit 0 is below the marker (never decides a min) and is shifted out
-// before anything reads it.  SDWA: shift each pad in place with v_lshrrev_b16 SDWA.
-template <int PH, int KIND, int MODE, bool SDWA>
-__device__ __forceinline__ void column4(uint32_t& M0, uint32_t& M1, uint32_t P, const Consts& K) {
-  uint32_t T0, T1;
-  if constexpr (MODE == 1) {
-    T0 = M0 & 0xFF00FF00u;
-    T1 = M1 & 0xFF00FF00u;
-  } else if constexpr (SDWA) {
-    T0 = M0; T1 = M1;
-    asm("v_lshrrev_b16_sdwa %0, 1, %0 dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src1_sel:WORD_0\n\t"
-        "v_lshrrev_b16_sdwa %0, 1, %0 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src1_sel:WORD_1"
-        : "+v"(T0));
-    asm("v_lshrrev_b16_sdwa %0, 1, %0 dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src1_sel:WORD_0\n\t"
-        "v_lshrrev_b16_sdwa %0, 1, %0 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src1_sel:WORD_1"
-        : "+v"(T1));
-  } else {
-    T0 = ((M0 >> 1) & 0x00FF00FFu) | (M0 & 0xFF00FF00u);
-    T1 = ((M1 >> 1) & 0x00FF00FFu) | (M1 & 0xFF00FF00u);
+template <int PH, int D>
+__device__ __forceinline__ void column_acs(uint32_t (&M)[kDw], const uint32_t (&T)[kDw], const uint32_t (&BX)[kDw],
+                                           const uint32_t (&BY)[kDw]) {
+  constexpr int pb = 5 - PH;                           // partner's position bit
+  const uint32_t X = T[D] + BX[D];
+  uint32_t Z;
+  if constexpr (pb == 0) {         // partner = the other half: [T.lo + BY.hi][T.hi + BY.lo] in one op
+    asm("v_pk_add_u16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(Z) : "v"(T[D]), "v"(BY[D]));
+  } else if constexpr (pb <= kDwBits) {                // partner = another dword of the lane
+    Z = T[D ^ (1 << (pb - 1))] + BY[D];
+  } else {                                             // partner lane: the DPP source of the add
+    Z = (uint32_t)__builtin_amdgcn_mov_dpp((int)T[D], partner_dpp(pb), 0xF, 0xF, true) + BY[D];
   }
-  constexpr uint32_t C = KIND == 0 ? 0x1C801C80u : 0x0E800E80u;
-  const uint32_t BX0 = __builtin_amdgcn_perm(0x80808080u, P, K.sel[PH][0]);
-  const uint32_t BX1 = __builtin_amdgcn_perm(0x80808080u, P, K.sel[PH][1]);
-  const uint32_t BY0 = C - BX0, BY1 = C - BX1;
-  auto add = [](uint32_t a, uint32_t b) -> uint32_t {
-    if constexpr (MODE == 2) return w32(h2(a) + h2(b));
-    else return a + b;
-  };
-  const uint32_t X0 = add(T0, BX0), X1 = add(T1, BX1);
-  uint32_t Z0, Z1;
-  if constexpr (PH <= 3) {
-    constexpr int ctrl = PH == 0 ? 0x128 : PH == 1 ? 0x140 : PH == 2 ? 0x4E : 0xB1;  // xor 8, 15, 2, 1
-    Z0 = add((uint32_t)__builtin_amdgcn_mov_dpp((int)T0, ctrl, 0xF, 0xF, true), BY0);
-    Z1 = add((uint32_t)__builtin_amdgcn_mov_dpp((int)T1, ctrl, 0xF, 0xF, true), BY1);
-  } else if constexpr (PH == 4) {
-    Z0 = add(T1, BY0);
-    Z1 = add(T0, BY1);
-  } else {
-    Z0 = w32(h2(T0).yx + h2(BY0));
-    Z1 = w32(h2(T1).yx + h2(BY1));
-  }
-  M0 = w32(__builtin_elementwise_min(h2(X0), h2(Z0)));
-  M1 = w32(__builtin_elementwise_min(h2(X1), h2(Z1)));
+  M[D] = w32(__builtin_elementwise_min(h2(X), h2(Z)));
 }
-
-// Shift-free column (tests/vit3_model.py Packet.step5).  The column with cycle phase KPH =
-// (c + 1) mod 8 (c = the column computed; KPH 7 is the snapshot column) writes its marker at
-// bit KPH + 1 of each half: a half is [H >> 1 in bits 15..9][the cycle's decisions in bits
-// 8..1, oldest lowest][bit 0: carry guard].  Bits above the marker are still 0 in both
-// candidates (cleared at KPH 0), so the marker breaks ties exactly like the brick's metric
-// LSB (viterbicore.hpp:105-147), and the pads need no shift: one AND per dword clears the
-// guard bit 16 that a 32-bit add carries into when H0 wraps (at KPH 0 it also clears the
-// cycle's history).  At KPH 7 the marker is bit 8, the LSB of the (even) H byte: BX =
-// [BM][bm << 7] plus its own low byte = [BM + bm][0].
-template <int PH, int KIND, int KPH>
-__device__ __forceinline__ void column5(uint32_t& M0, uint32_t& M1, uint32_t P, const Consts& K) {
+template <int PH, int KIND, int KPH, int... D>
+__device__ __forceinline__ void column5_(uint32_t (&M)[kDw], uint32_t P, const Consts& K, std::integer_sequence<int, D...>) {
   constexpr uint32_t mask = KPH == 0 ? 0xFE00FE00u : 0xFFFEFFFFu;
-  const uint32_t T0 = M0 & mask, T1 = M1 & mask;
+  const uint32_t T[kDw] = {(M[D] & mask)...};
   constexpr uint32_t mk = 2u << KPH;
   constexpr uint32_t Kc = KIND == 0 ? 28u : 14u;
   constexpr uint32_t C = KPH == 7 ? ((Kc + 1u) << 8) * 0x00010001u : ((Kc << 8) | mk) * 0x00010001u;
-  // Dword 1 holds dword 0's positions with position bit 1 set, i.e. state bit (1 + PH) % 6
-  // flipped: at PH 2 that is state bit 3, which changes neither expected bit nor the
-  // marker (BX1 = BX0); at PH 4 it is bit 5, the marker only (BX1 = BX0 ^ marker bits).
-  // tests/test_vit3_model.py checks both selector identities.
-  constexpr uint32_t mbits = KPH == 7 ? 0x01000100u : mk * 0x00010001u;
-  uint32_t BX0, BX1;
-  if constexpr (KPH == 7) {        // [BM + bm][0] per half: BM (even) or BM + 1 = byte of P | 0x01010101
-    static_assert(PH & 1, "KPH 7 columns have odd phases (body columns 5, 13, 21)");
-    const uint32_t P1 = P | 0x01010101u;
-    BX0 = __builtin_amdgcn_perm(P1, P, K.sel7[PH >> 1][0]);
-    BX1 = __builtin_amdgcn_perm(P1, P, K.sel7[PH >> 1][1]);
-  } else {
-    BX0 = __builtin_amdgcn_perm((mk & 0xFFu) * 0x01010101u, P, K.sel[PH][0]);
-    if constexpr (PH == 2) BX1 = BX0;
-    else if constexpr (PH == 4) BX1 = BX0 ^ mbits;
-    else BX1 = __builtin_amdgcn_perm((mk & 0xFFu) * 0x01010101u, P, K.sel[PH][1]);
-  }
-  // Keep C - BX a value of its own: reassociated as (partner T - BX) + C it would put two
-  // adds after the AND on the column-to-column dependency chain instead of one (a wave
-  // alone on its SIMD waits out that chain every column).
-  uint32_t BY0 = C - BX0;
-  asm("" : "+v"(BY0));
-  uint32_t BY1 = BY0;
-  if constexpr (PH != 2) {
-    BY1 = C - BX1;
-    asm("" : "+v"(BY1));
-  }
-  const uint32_t X0 = T0 + BX0, X1 = T1 + BX1;
-  uint32_t Z0, Z1;
-  if constexpr (PH <= 3) {
-    constexpr int ctrl = PH == 0 ? 0x128 : PH == 1 ? 0x140 : PH == 2 ? 0x4E : 0xB1;  // xor 8, 15, 2, 1
-    Z0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)T0, ctrl, 0xF, 0xF, true) + BY0;
-    Z1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)T1, ctrl, 0xF, 0xF, true) + BY1;
-  } else if constexpr (PH == 4) {
-    Z0 = T1 + BY0;
-    Z1 = T0 + BY1;
-  } else {                         // partner = the other half: [T.lo + BY.hi][T.hi + BY.lo] in one op
-    asm("v_pk_add_u16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(Z0) : "v"(T0), "v"(BY0));
-    asm("v_pk_add_u16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(Z1) : "v"(T1), "v"(BY1));
-  }
-  M0 = w32(__builtin_elementwise_min(h2(X0), h2(Z0)));
-  M1 = w32(__builtin_elementwise_min(h2(X1), h2(Z1)));
+  uint32_t BX[kDw], BY[kDw];
+  (column_bx<PH, KPH, D>(BX, BY, P, K, C), ...);
+  (column_acs<PH, D>(M, T, BX, BY), ...);
+}
+template <int PH, int KIND, int KPH>
+__device__ __forceinline__ void column5(uint32_t (&M)[kDw], uint32_t P, const Consts& K) {
+  column5_<PH, KIND, KPH>(M, P, K, std::make_integer_sequence<int, kDw>{});
 }
 
 // normalize (viterbicore.hpp:149-168): H -= min over the row's 64 H bytes (H even).
-__device__ __forceinline__ void normalize(uint32_t& M0, uint32_t& M1) {
-  const u16x2 t = __builtin_elementwise_min(h2(M0), h2(M1));
+__device__ __forceinline__ void normalize(uint32_t (&M)[kDw]) {
+  u16x2 t = h2(M[0]);
+#pragma unroll
+  for (int d = 1; d < kDw; d++) t = __builtin_elementwise_min(t, h2(M[d]));
   uint32_t v = (uint32_t)min(t.x, t.y);
   v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
   v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
   v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));
-  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false));
+  if constexpr (kLanes == 16) v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false));
   const uint32_t rep = __builtin_amdgcn_perm(0u, v, 0x010C010Cu);   // [H][0][H][0]
-  M0 = w32(h2(M0) - h2(rep));
-  M1 = w32(h2(M1) - h2(rep));
+#pragma unroll
+  for (int d = 0; d < kDw; d++) M[d] = w32(h2(M[d]) - h2(rep));
+}
+// min / max of a row-uniform value over the wave's rows (scalar)
+__device__ __forceinline__ uint32_t wave_min_rows(uint32_t v) {
+  uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+#pragma unroll
+  for (int r = 1; r < kRowsWave; r++) m = min(m, (uint32_t)__builtin_amdgcn_readlane((int)v, r * kLanes));
+  return m;
 }
 
 // 64-bit value of `lane` as a wave-uniform scalar
@@ -306,7 +293,7 @@ constexpr uint32_t kSegCmp = 240;                      // S_k -> C_k
 constexpr int kMaxSeg = 8;
 constexpr uint32_t kMinSeg = 1536;                     // columns per segment at least
 constexpr uint32_t kSegMaxEnd = 1u << 24;              // longer frames are not split
-constexpr uint32_t kSeamWords = 32;                    // uint2 per dump: 16 lanes x (M0, M1)
+constexpr uint32_t kSeamWords = 32;                    // uint2 per dump slot (kLanes x kDw / 2 used: 16)
 // Segment length of a mixed batch: L x kSegMixNum / 8, L = the batch's columns / (64 rows
 // per CU); the launch grid allows 8 / kSegMixNum x 64 rows per CU + one per packet.
 // Measured on config 5 (interleaved A/B, 3 rounds): 4/8 L 0.62 ms Viterbi, 6/8 0.585, 8/8
@@ -327,18 +314,18 @@ __host__ __device__ __forceinline__ uint32_t udiv_small(uint32_t y, uint32_t n) 
 __host__ __device__ __forceinline__ uint32_t udiv_rcp(uint32_t b, uint32_t rcp) {
   return (uint32_t)(((uint64_t)b * rcp) >> 32);
 }
-// Sorted position -> row slot: the nfull whole blocks of 16 rows placed "snake" over ncu
+// Sorted position -> row slot: the nfull whole blocks of kRows rows placed "snake" over ncu
 // CUs: in odd rounds of ncu blocks the order is reversed, so with blocks dealt to CU
 // (slot mod ncu) — what the dispatcher does when every block of the launch is resident
 // (scripts/ubench/hwid.hip) — the CU running one of the longest blocks gets one of the
 // shortest of the next round beside it.  An involution within each round; a partial last
 // block stays in place.  rcp = 0xFFFFFFFF / ncu + 1 (ncu >= 2).
 __host__ __device__ __forceinline__ uint32_t order_place(uint32_t pos, uint32_t nfull, uint32_t ncu, uint32_t rcp) {
-  const uint32_t b = pos >> 4;
+  const uint32_t b = pos / (uint32_t)kRows;
   if (b >= nfull) return pos;
   const uint32_t r = udiv_rcp(b, rcp), c = b - r * ncu, base = r * ncu;
   const uint32_t m = min(ncu, nfull - base);
-  return ((r & 1u) ? base + m - 1u - c : b) * 16u + (pos & 15u);
+  return ((r & 1u) ? base + m - 1u - c : b) * (uint32_t)kRows + pos % (uint32_t)kRows;
 }
 // The plan header k_pkt_plan writes for k_viterbi3 (int32 words of the nrows buffer).
 enum PlanWord { kPlanRows = 0, kPlanFixes = 1, kPlanUniform = 2, kPlanNcu = 3, kPlanSegLen = 4, kPlanDropped = 5 };   // (8 words)
@@ -380,7 +367,7 @@ struct Row {
   bool live;                          // still decoding (not done, input not exhausted)
   bool ppend, fpend;                  // partial / final traceback due at the body end
   uint32_t pT, plook, fT, fcnt, flook;
-  uint32_t pM0, pM1, fM0, fM1;
+  uint32_t pM[kDw], fM[kDw];
   uint32_t nbytes;                    // bytes written so far
 };
 
@@ -388,11 +375,37 @@ __device__ __forceinline__ uint32_t row_next(const Row& R) {
   if (!R.live) return kNever;
   return min(min(R.ob + 286u, R.end), min(R.cols, R.evc));
 }
+// the lanes of this lane's row in a wave ballot, shifted down to bit 0
+__device__ __forceinline__ uint32_t row_bits(uint64_t ballot) {
+  return (uint32_t)(ballot >> (__lane_id() & (64u - kLanes))) & kRowMask;
+}
+// a seam dump: the row's 64 metric halves, kDw / 2 uint2 per lane
+__device__ __forceinline__ void dump_store(uint2* __restrict__ at, uint32_t l, const uint32_t (&M)[kDw]) {
+#pragma unroll
+  for (int i = 0; i < kDw / 2; i++) at[(kDw / 2) * l + i] = make_uint2(M[2 * i], M[2 * i + 1]);
+}
+__device__ __forceinline__ void dump_load(const uint2* __restrict__ at, uint32_t l, uint32_t (&M)[kDw]) {
+#pragma unroll
+  for (int i = 0; i < kDw / 2; i++) {
+    const uint2 v = at[(kDw / 2) * l + i];
+    M[2 * i] = v.x; M[2 * i + 1] = v.y;
+  }
+}
+// do the H bits (& 0xFE00FE00) of two dumps differ in this lane?
+__device__ __forceinline__ bool dump_ne(const uint2* __restrict__ a, const uint2* __restrict__ b, uint32_t l) {
+  uint32_t x = 0;
+#pragma unroll
+  for (int i = 0; i < kDw / 2; i++) {
+    const uint2 u = a[(kDw / 2) * l + i], v = b[(kDw / 2) * l + i];
+    x |= (u.x ^ v.x) | (u.y ^ v.y);
+  }
+  return (x & 0xFE00FE00u) != 0u;
+}
 
 // Seam event of a row at relative column tr (a body end, after normalize): a segment stores
 // its metrics for the fix pass; a fix row compares its own with the next segment's start
 // state and, when they agree, stops where that segment's windows begin.
-__device__ __forceinline__ void seam_event(Row& R, uint32_t tr, uint32_t M0, uint32_t M1, uint32_t l, uint32_t rib,
+__device__ __forceinline__ void seam_event(Row& R, uint32_t tr, const uint32_t (&M)[kDw], uint32_t l, uint32_t rib,
                                         RowX* rowx, uint2* __restrict__ dumps) {
   RowX x = rowx[rib];
   const uint32_t k = x.kn & 0xFFu, nseg = (x.kn >> 8) & 0xFFu, fix = (x.kn >> 16) & 1u, j = x.kn >> 20;
@@ -407,7 +420,7 @@ __device__ __forceinline__ void seam_event(Row& R, uint32_t tr, uint32_t M0, uin
 #endif
   if (!fix) {
     const uint32_t side = j == k ? 1u : 0u;            // at C_k: segment k's start; at C_{k+1}: its end side
-    dumps[seam_index(x.p, j, side) + l] = make_uint2(M0, M1);
+    dump_store(dumps + seam_index(x.p, j, side), l, M);
     if (side == 1u && k + 1u < nseg) {
       x.kn = (x.kn & 0xFFFFFu) | ((k + 1u) << 20);
       R.evc = seg_start(x.E, nseg, k + 1u) + kSegCmp - x.S;
@@ -415,10 +428,13 @@ __device__ __forceinline__ void seam_event(Row& R, uint32_t tr, uint32_t M0, uin
       R.evc = kNever;
     }
   } else {
-    const uint2 b = dumps[seam_index(x.p, j, 1u) + l];
-    const bool ne = (((M0 ^ b.x) | (M1 ^ b.y)) & 0xFE00FE00u) != 0u;
-    const uint64_t bad = __builtin_amdgcn_ballot_w64(ne);
-    if (((bad >> (__lane_id() & 48u)) & 0xFFFFu) == 0u) {   // the row's 64 H bytes agree
+    uint32_t B[kDw];
+    dump_load(dumps + seam_index(x.p, j, 1u), l, B);
+    uint32_t d = 0;
+#pragma unroll
+    for (int i = 0; i < kDw; i++) d |= M[i] ^ B[i];
+    const uint64_t bad = __builtin_amdgcn_ballot_w64((d & 0xFE00FE00u) != 0u);
+    if (row_bits(bad) == 0u) {                         // the row's 64 H bytes agree
       R.cols = min(R.cols, seg_start(x.E, nseg, j) + kSegWarm + 30u - x.S);
       x.kn |= 1u << 17;
       R.evc = kNever;
@@ -431,21 +447,20 @@ __device__ __forceinline__ void seam_event(Row& R, uint32_t tr, uint32_t M0, uin
   }
   rowx[rib] = x;
 }
-__device__ __forceinline__ uint32_t wave_min_rows(uint32_t v) {
-  const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 0), b = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
-  const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)v, 32), d = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
-  return min(min(a, b), min(c, d));
-}
 
 // Events after a group ending at column tr (sora_ext_viterbi.cpp:112-149); normalize ran first.
-__device__ __forceinline__ void events(Row& R, uint32_t tr, uint32_t M0, uint32_t M1) {
+__device__ __forceinline__ void events(Row& R, uint32_t tr, const uint32_t (&M)[kDw]) {
   if (R.live && tr >= R.next) {
     if (tr >= R.end) {                                  // final traceback
-      R.fpend = true; R.fM0 = M0; R.fM1 = M1; R.fT = tr;
+      R.fpend = true; R.fT = tr;
+#pragma unroll
+      for (int d = 0; d < kDw; d++) R.fM[d] = M[d];
       R.fcnt = R.end - R.ob - 6u; R.flook = tr - R.end;
       R.live = false;
     } else if (tr >= R.ob + 286u) {                     // 256 bits, lookahead 24 + (tr-thresh)%8
-      R.ppend = true; R.pM0 = M0; R.pM1 = M1; R.pT = tr;
+      R.ppend = true; R.pT = tr;
+#pragma unroll
+      for (int d = 0; d < kDw; d++) R.pM[d] = M[d];
       R.plook = 24u + ((tr - (R.ob + 286u)) & 7u);
       R.ob += 256u;
     }
@@ -506,33 +521,28 @@ __device__ __forceinline__ void walk_finish(Walk& W, const uint8_t* ring0, uint3
 // DEFER (partial windows): rows sharing a window leave the window's last 24 or 16 output
 // bytes to the next body's columns (W); tr0 is the first column of the body that raised the
 // event.
-template <bool V5, bool DEFER = false>
-__device__ __forceinline__ void traceback(bool due, uint32_t M0, uint32_t M1, uint32_t T, uint32_t cnt,
+template <bool DEFER = false>
+__device__ __forceinline__ void traceback(bool due, const uint32_t (&M)[kDw], uint32_t T, uint32_t cnt,
                                           uint32_t look, uint32_t l, uint32_t rib, const uint8_t* ring,
                                           uint8_t* __restrict__ out, uint32_t ooff, uint32_t& nbytes,
                                           Walk* W = nullptr, uint32_t tr0 = 0) {
   const uint32_t ph = T % 6u;
   uint32_t best = 0xFFFFFFFFu;
 #pragma unroll
-  for (int q = 0; q < 4; q++) {
-    const uint32_t half = ((q >> 1) ? M1 : M0) >> (16 * (q & 1)) & 0xFFFFu;
+  for (int q = 0; q < 2 * kDw; q++) {
+    const uint32_t half = M[q >> 1] >> (16 * (q & 1)) & 0xFFFFu;
     const uint32_t st = rotl6(pos_of(l, q >> 1, q & 1), ph);
-    uint32_t m, pad;
-    if constexpr (V5) {   // marker of column T at bit (T+1)%8 + 1; the n = (T-6)%8 newest decisions in bits n..1
-      const uint32_t n = (T - 6u) & 7u;
-      m = ((half >> 8) & 0xFEu) | ((half >> (((T + 1u) & 7u) + 1u)) & 1u);
-      pad = (((half >> 1) & ((1u << n) - 1u)) << (8u - n)) & 0xFFu;   // as the shifted pad: newest at bit 7
-    } else {
-      m = (half >> 8) | ((half >> 7) & 1u);
-      pad = half & 0xFFu;
-    }
+    // marker of column T at bit (T+1)%8 + 1; the n = (T-6)%8 newest decisions in bits n..1
+    const uint32_t n = (T - 6u) & 7u;
+    const uint32_t m = ((half >> 8) & 0xFEu) | ((half >> (((T + 1u) & 7u) + 1u)) & 1u);
+    const uint32_t pad = (((half >> 1) & ((1u << n) - 1u)) << (8u - n)) & 0xFFu;   // as the shifted pad: newest at bit 7
     const uint32_t ukey = (((m << 8) | (st << 2)) & 0xFFFFu) ^ 0x8000u;   // signed int16 order
     best = min(best, (ukey << 16) | pad);
   }
   best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0xB1, 0xF, 0xF, false));
   best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x4E, 0xF, 0xF, false));
   best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x141, 0xF, 0xF, false));
-  best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x140, 0xF, 0xF, false));
+  if constexpr (kLanes == 16) best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x140, 0xF, 0xF, false));
   const bool walker = due && l == 0 && cnt != 0;
   const uint64_t wm = __builtin_amdgcn_ballot_w64(walker);
   if (wm == 0) return;
@@ -643,15 +653,16 @@ __device__ __forceinline__ uint32_t p_word(const PKind& k, uint32_t a, uint32_t 
 
 // DBG (timing experiments only, never selected by default): 1 skip the traceback walk,
 // 2 skip snapshot stores, 4 skip normalization, 8 no P broadcast, 16 never run checked bodies,
-// 32 broadcast P with DPP row_newbcast, 64 ds_swizzle issued 4 columns ahead behind a
-// scheduling barrier, 128 the v3 column (packed adds + v_mov_dpp), 256 SDWA pad shifts,
-// 512 the shifted-pad 32-bit-add column (column4, the previous default), 1024 no soft fetch
-// (every body reuses the first body's soft values).  128/256/512 are exact (other layouts),
-// the rest are timing-only.
+// 64 ds_swizzle issued 4 columns ahead behind a scheduling barrier, 1024 no soft fetch
+// (every body reuses the first body's soft values).  All are timing-only (wrong output).
+constexpr int kPw = (24 + kLanes - 1) / kLanes;        // P words a lane builds per body (3 or 2)
+#ifndef ZRX_VPF
+#define ZRX_VPF 1
+#endif
+constexpr int kPf = ZRX_VPF;                           // bodies the soft-value fetch runs ahead
 template <int CR, int DBG = 0>
 struct Packet {
   using RT = Rate<CR>;
-  static constexpr bool V5 = (DBG & (128 | 256 | 512)) == 0;   // shift-free column (default)
   const Consts& K;
   Row& R;
   uint32_t l, rib;
@@ -661,12 +672,10 @@ struct Packet {
   RowX* rowx;                                          // the block's cold row facts (seam events)
   uint2* dumps;                                        // seam dumps
 
+  // P word of body column J: lane J mod kLanes of the row built it as its word J / kLanes
   template <int J>
-  static __device__ __forceinline__ uint32_t bcast(uint32_t Pa, uint32_t Pb) {   // P word of body column J
-    if constexpr ((DBG & 32) != 0)
-      return (uint32_t)__builtin_amdgcn_mov_dpp((int)(J < 16 ? Pa : Pb), 0x150 + (J & 15), 0xF, 0xF, false);
-    else
-      return (uint32_t)__builtin_amdgcn_ds_swizzle((int)(J < 16 ? Pa : Pb), ((J & 15) << 5) | 0x10);
+  static __device__ __forceinline__ uint32_t bcast(const uint32_t (&Pw)[kPw]) {
+    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)Pw[J / kLanes], ((J % kLanes) << 5) | (32 - kLanes));
   }
   // The deferred traceback steps of column J (branch-free; see Walk): steps 2J, 2J + 1 in
   // columns 0..11, step J + 12 after, NL + 32 steps in all.
@@ -679,72 +688,73 @@ struct Packet {
       walk_stepk(*W, (uint32_t)(J + 12), (uint32_t)NL, ring0, rib * 64u);
     }
   }
+  template <uint32_t O>
+static __device__ __forceinline__ void ds_b8(uint32_t a, uint32_t v) {
+  asm volatile("ds_write_b8 %0, %1 offset:%2" ::"v"(a), "v"(v), "i"(O) : "memory");
+}
+template <uint32_t O>
+static __device__ __forceinline__ void ds_b8_hi(uint32_t a, uint32_t v) {
+  asm volatile("ds_write_b8_d16_hi %0, %1 offset:%2" ::"v"(a), "v"(v), "i"(O) : "memory");
+}
+// Snapshot k (column C = 8k + 6 of the body, C mod 6 = 2k): every position's pad byte
+  // (bits 8..1 of its half) to the ring at the lane's first offset plus a lane-uniform delta.
+  template <int k, int... D>
+  __device__ __forceinline__ void snapshot(const uint32_t (&M)[kDw], std::integer_sequence<int, D...>) {
+    uint8_t* s = ring + k * kSlotBytes;
+    const uint32_t u[kDw] = {(M[D] >> 1)...};
+    if constexpr (k == 2) {
+      // C mod 6 = 4: position bits 0, 1 go to ring-index bits 1, 0, so (dword pair, half)
+      // are 4 consecutive ring bytes, byte (h << 1) | (d & 1): one dword store per pair
+      static_assert(snap_delta(2, 1, 0) == 1 && snap_delta(2, 0, 1) == 2, "k = 2 byte order");
+#pragma unroll
+      for (int e = 0; e < kDw / 2; e++)
+        *(uint32_t*)(s + K.sa[2] + snap_delta(2, 2 * e, 0)) = __builtin_amdgcn_perm(u[2 * e + 1], u[2 * e], 0x06020400u);
+    } else {
+      // one address register serves all stores through their offsets: half 0 by
+      // ds_write_b8, half 1 by ds_write_b8_d16_hi
+      const uint32_t a = lds_addr(s) + K.sa[k];
+      (ds_b8<snap_delta(k, D, 0)>(a, u[D]), ...);
+      (ds_b8_hi<snap_delta(k, D, 1)>(a, u[D]), ...);
+    }
+  }
   template <int J, bool CHECKED, int WE>
-  __device__ __forceinline__ void col(uint32_t& M0, uint32_t& M1, uint32_t (&Pq)[4], uint32_t Pa, uint32_t Pb,
+  __device__ __forceinline__ void col(uint32_t (&M)[kDw], uint32_t (&Pq)[4], const uint32_t (&Pw)[kPw],
                                       uint32_t tr0, uint32_t& s_next) {
     if constexpr (WE > 0) walk_col<J, WE>();
     uint32_t P;
     if constexpr ((DBG & 8) != 0) {
-      P = J < 16 ? Pa : Pb;
-    } else if constexpr ((DBG & 32) != 0) {
-      P = bcast<J>(Pa, Pb);
+      P = Pw[J / kLanes];
     } else {
       P = Pq[J & 3];
-      if constexpr (J + 4 < 24) Pq[J & 3] = bcast<J + 4>(Pa, Pb);   // issued 4 columns ahead
+      if constexpr (J + 4 < 24) Pq[J & 3] = bcast<J + 4>(Pw);   // issued 4 columns ahead
       if constexpr ((DBG & 64) != 0) __builtin_amdgcn_sched_barrier(0);
     }
     constexpr int r = J % RT::steps;
     constexpr int c = J + 1;                           // column index within the body after the step
-    if constexpr (V5)
-      column5<J % 6, r, (J + 2) % 8>(M0, M1, P, K);
-    else if constexpr ((DBG & 128) != 0)
-      column<J % 6, r>(M0, M1, P, K);
-    else
-      column4<J % 6, r, c % 8 == 6 ? 2 : c % 8 == 7 ? 1 : 0, (DBG & 256) != 0>(M0, M1, P, K);
-    if constexpr (c % 8 == 6 && !(DBG & 2)) {          // snapshot column (C = 6 mod 8)
-      uint8_t* s = ring + (c >> 3) * kSlotBytes;
-      constexpr int sh = V5 ? 1 : 0;                   // v5: the decisions are bits 8..1
-      const uint32_t u0 = M0 >> sh, u1 = M1 >> sh;
-      if constexpr (V5 && (c >> 3) == 2) {
-        // C mod 6 = 4: the lane's 4 states are 4 consecutive ring bytes, byte (h << 1) | d
-        // (rev6(rotl6(p, 4)) sends position bits 0, 1 to ring-index bits 1, 0): one dword store
-        *(uint32_t*)(s + K.sa2w) = __builtin_amdgcn_perm(u1, u0, 0x06020400u);
-      } else {
-        // The lane's 4 ring bytes differ from its first by lane-uniform amounts (position
-        // bit 0 = half -> ring-index bit 5 - 2k, bit 1 = dword -> bit 4 - 2k, k = C mod 6 / 2),
-        // so one address register serves all four stores through their offsets.  One shift
-        // per dword: byte 0 by ds_write_b8, byte 2 by ds_write_b8_d16_hi.
-        constexpr uint32_t k = (uint32_t)(c >> 3), o = k * kSlotBytes;
-        constexpr uint32_t dh = 32u >> (2 * k), dd = 16u >> (2 * k);
-        const uint32_t a = lds_addr(ring) + K.sa[k][0];
-        asm volatile("ds_write_b8 %0, %1 offset:%2" ::"v"(a), "v"(u0), "i"(o) : "memory");
-        asm volatile("ds_write_b8 %0, %1 offset:%2" ::"v"(a), "v"(u1), "i"(o + dd) : "memory");
-        asm volatile("ds_write_b8_d16_hi %0, %1 offset:%2" ::"v"(a), "v"(u0), "i"(o + dh) : "memory");
-        asm volatile("ds_write_b8_d16_hi %0, %1 offset:%2" ::"v"(a), "v"(u1), "i"(o + dh + dd) : "memory");
-      }
-    }
+    column5<J % 6, r, (J + 2) % 8>(M, P, K);
+    if constexpr (c % 8 == 6 && !(DBG & 2)) snapshot<(c >> 3)>(M, std::make_integer_sequence<int, kDw>{});
     if constexpr (c % RT::steps == 0) {                // group end
-      if constexpr (c % 8 == 0 && (CR != 2 || c == 24) && !(DBG & 4)) normalize(M0, M1);
+      if constexpr (c % 8 == 0 && (CR != 2 || c == 24) && !(DBG & 4)) normalize(M);
       if constexpr (CHECKED) {
         const uint32_t tr = tr0 + c;
         if (tr >= s_next) {
           // seam events sit on body ends (seam columns are multiples of 24 from the row's start)
           if constexpr (c == 24)
-            if (R.live && tr == R.evc) seam_event(R, tr, M0, M1, l, rib, rowx, dumps);
-          events(R, tr, M0, M1);
+            if (R.live && tr == R.evc) seam_event(R, tr, M, l, rib, rowx, dumps);
+          events(R, tr, M);
           s_next = wave_min_rows(R.next);
         }
       }
     }
   }
   template <bool CHECKED, int WE, int... J>
-  __device__ __forceinline__ void body(uint32_t& M0, uint32_t& M1, uint32_t Pa, uint32_t Pb, uint32_t tr0,
-                                       uint32_t& s_next, std::integer_sequence<int, J...>) {
+  __device__ __forceinline__ void body(uint32_t (&M)[kDw], const uint32_t (&Pw)[kPw], uint32_t tr0, uint32_t& s_next,
+                                       std::integer_sequence<int, J...>) {
     uint32_t Pq[4] = {0, 0, 0, 0};
-    if constexpr (!(DBG & 40)) {
-      Pq[0] = bcast<0>(Pa, Pb); Pq[1] = bcast<1>(Pa, Pb); Pq[2] = bcast<2>(Pa, Pb); Pq[3] = bcast<3>(Pa, Pb);
+    if constexpr (!(DBG & 8)) {
+      Pq[0] = bcast<0>(Pw); Pq[1] = bcast<1>(Pw); Pq[2] = bcast<2>(Pw); Pq[3] = bcast<3>(Pw);
     }
-    (col<J, CHECKED, WE>(M0, M1, Pq, Pa, Pb, tr0, s_next), ...);
+    (col<J, CHECKED, WE>(M, Pq, Pw, tr0, s_next), ...);
   }
 };
 
@@ -756,10 +766,24 @@ __device__ __forceinline__ uint32_t soft_off(uint32_t j) {
   return g * G + (r == 0 ? 0u : r + 1u);
 }
 
+// min / max of a row-uniform 64-bit value over the wave's rows (scalar)
+__device__ __forceinline__ int64_t wave_min_rows64(int64_t v) {
+  int64_t m = rl64(v, 0);
+#pragma unroll
+  for (int r = 1; r < kRowsWave; r++) m = min(m, rl64(v, r * kLanes));
+  return m;
+}
+__device__ __forceinline__ int64_t wave_max_rows64(int64_t v) {
+  int64_t m = rl64(v, 0);
+#pragma unroll
+  for (int r = 1; r < kRowsWave; r++) m = max(m, rl64(v, r * kLanes));
+  return m;
+}
+
 template <int CR, int DBG>
 __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64_t so, uint32_t n, Row& R, const Consts& K, uint32_t l,
                          uint32_t rib, uint8_t* ring_block, uint8_t* __restrict__ out, uint32_t ooff,
-                         uint32_t M0, uint32_t M1, RowX* rowx, uint2* __restrict__ dumps) {
+                         uint32_t (&M)[kDw], RowX* rowx, uint2* __restrict__ dumps) {
   using RT = Rate<CR>;
   Walk W;
   W.we = 0;
@@ -768,11 +792,16 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
   W.voff = 0x80000000u;
   W.ob = (uint64_t)(uintptr_t)out;
   Packet<CR, DBG> pk{K, R, l, rib, ring_block, ring_block, &W, rowx, dumps};
-  // this lane builds the P words of body columns j1 = l and j2 = 16 + l (l < 8)
-  const uint32_t j1 = l, j2 = 16u + (l & 7u);
-  const uint32_t o1 = soft_off<CR>(j1), o2 = soft_off<CR>(j2);
-  const uint32_t r1 = j1 % RT::steps, r2 = j2 % RT::steps;
-  const PKind k1 = p_kind(r1), k2 = p_kind(r2);
+  // this lane builds the P words of body columns kLanes i + l (i < kPw; 16-lane rows: the
+  // second word of lanes 8..15 repeats lanes 0..7's)
+  uint32_t vo[kPw];
+  PKind kd[kPw];
+#pragma unroll
+  for (int i = 0; i < kPw; i++) {
+    const uint32_t j = kLanes * i + ((kLanes * i + l < 24u) ? l : (l & 7u));
+    vo[i] = soft_off<CR>(j);
+    kd[i] = p_kind(j % RT::steps);
+  }
   // Soft values by buffer loads: one wave-uniform descriptor over the rows' soft windows,
   // advanced by the scalar unit every body, and a per-lane byte offset that never changes
   // (row offset + column offset; b at offset:1).  Reads past the furthest row's last soft
@@ -780,25 +809,41 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
   // neighbour's values, which feed only columns beyond R.cols.  The caller (k_viterbi3)
   // passes rows whose soft values lie within kSoftWindow of each other.
   const int64_t lo_me = R.live ? so : INT64_MAX, hi_me = R.live ? so + (int64_t)n : INT64_MIN;
-  const int64_t lo_w = min(min(rl64(lo_me, 0), rl64(lo_me, 16)), min(rl64(lo_me, 32), rl64(lo_me, 48)));
-  const int64_t hi_w = max(max(rl64(hi_me, 0), rl64(hi_me, 16)), max(rl64(hi_me, 32), rl64(hi_me, 48)));
+  const int64_t lo_w = wave_min_rows64(lo_me);
+  const int64_t hi_w = wave_max_rows64(hi_me);
   if (hi_w - lo_w > kSoftWindow) {                     // one row's soft values beyond 4 GiB: not decodable
     if (R.live) R.nbytes = 0xFFFFFFFFu;
     return;
   }
   const uint32_t rel = R.live ? (uint32_t)(so - lo_w) : 0u;
-  const uint32_t v1 = rel + o1, v2 = rel + o2;
-  auto fetch = [&](uint32_t base, uint32_t& a1_, uint32_t& b1_, uint32_t& a2_, uint32_t& b2_) {
+#pragma unroll
+  for (int i = 0; i < kPw; i++) vo[i] += rel;
+  // soft bytes of the next kPf bodies in flight (sa[0]: the next body's)
+  uint32_t sa[kPf][kPw], sb[kPf][kPw];
+  auto fetch_into = [&](uint32_t (&A)[kPw], uint32_t (&B)[kPw], uint32_t base) {
     const int64_t left = hi_w - lo_w - (int64_t)base;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(soft + lo_w + base), (short)0, (int)(uint32_t)(left > 0 ? left : 0), 0x00020000);
-    a1_ = __builtin_amdgcn_raw_buffer_load_b8(rs, (int)v1, 0, 0);
-    b1_ = __builtin_amdgcn_raw_buffer_load_b8(rs, (int)v1 + 1, 0, 0);
-    a2_ = __builtin_amdgcn_raw_buffer_load_b8(rs, (int)v2, 0, 0);
-    b2_ = __builtin_amdgcn_raw_buffer_load_b8(rs, (int)v2 + 1, 0, 0);
+#pragma unroll
+    for (int i = 0; i < kPw; i++) {
+      A[i] = __builtin_amdgcn_raw_buffer_load_b8(rs, (int)vo[i], 0, 0);
+      B[i] = __builtin_amdgcn_raw_buffer_load_b8(rs, (int)vo[i] + 1, 0, 0);
+    }
   };
-  uint32_t a1, b1, a2, b2;
-  fetch(0, a1, b1, a2, b2);
+  // P words of the body at `base` from sa[0], then the fetch window moves one body on
+  auto pwords = [&](uint32_t (&Pw)[kPw], uint32_t base_) {
+#pragma unroll
+    for (int i = 0; i < kPw; i++) Pw[i] = p_word(kd[i], sa[0][i], sb[0][i]);
+    if constexpr ((DBG & 1024) == 0) {
+#pragma unroll
+      for (int q = 0; q + 1 < kPf; q++)
+#pragma unroll
+        for (int i = 0; i < kPw; i++) { sa[q][i] = sa[q + 1][i]; sb[q][i] = sb[q + 1][i]; }
+      fetch_into(sa[kPf - 1], sb[kPf - 1], base_ + kPf * RT::chunk);   // (latency hidden behind kPf bodies)
+    }
+  };
+#pragma unroll
+  for (int q = 0; q < kPf; q++) fetch_into(sa[q], sb[q], q * RT::chunk);
   uint32_t s_next = wave_min_rows(R.next);
   uint32_t slot = 0;                                   // first slot of this body (3 per body)
   uint32_t tr0 = 0, base = 0;
@@ -812,10 +857,10 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
     // The hot loop: bodies with no event due, no deferred walk, nothing else on this path
     // (its own loop, so the register allocator keeps the loop-carried values in place).
     while ((DBG & 16) || (s_next > tr0 + 24 && s_next != kNever)) {
-      const uint32_t Pa = p_word(k1, a1, b1), Pb = p_word(k2, a2, b2);
-      if constexpr ((DBG & 1024) == 0) fetch(base + RT::chunk, a1, b1, a2, b2);   // next body (latency hidden)
+      uint32_t Pw[kPw];
+      pwords(Pw, base);
       pk.ring = ring_block + slot * kSlotBytes;
-      pk.template body<false, 0>(M0, M1, Pa, Pb, tr0, s_next, cols24);
+      pk.template body<false, 0>(M, Pw, tr0, s_next, cols24);
       next_body();
       if constexpr ((DBG & 16) != 0) {                 // no events: stop at the input's end
         if (tr0 >= R.cols) R.live = false;
@@ -826,34 +871,32 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
     if (s_next == kNever) break;                       // every row is done
     // A body with an event due: checked, then the tracebacks it raised.
     {
-      const uint32_t Pa = p_word(k1, a1, b1), Pb = p_word(k2, a2, b2);
-      if constexpr ((DBG & 1024) == 0) fetch(base + RT::chunk, a1, b1, a2, b2);
+      uint32_t Pw[kPw];
+      pwords(Pw, base);
       pk.ring = ring_block + slot * kSlotBytes;
-      pk.template body<true, 0>(M0, M1, Pa, Pb, tr0, s_next, cols24);
+      pk.template body<true, 0>(M, Pw, tr0, s_next, cols24);
     }
     if ((DBG & 1) == 0 && __builtin_amdgcn_ballot_w64(R.ppend) != 0) {
-      traceback<Packet<CR, DBG>::V5, Packet<CR, DBG>::V5>(R.ppend, R.pM0, R.pM1, R.pT, 256u, R.plook, l, rib,
-                                                           ring_block, out, ooff, R.nbytes, &W, tr0);
+      traceback<true>(R.ppend, R.pM, R.pT, 256u, R.plook, l, rib, ring_block, out, ooff, R.nbytes, &W, tr0);
       walk_uniform(W);
       R.ppend = false;
     }
     if ((DBG & 1) == 0 && __builtin_amdgcn_ballot_w64(R.fpend) != 0) {
-      traceback<Packet<CR, DBG>::V5>(R.fpend, R.fM0, R.fM1, R.fT, R.fcnt, R.flook, l, rib, ring_block, out, ooff, R.nbytes);
+      traceback(R.fpend, R.fM, R.fT, R.fcnt, R.flook, l, rib, ring_block, out, ooff, R.nbytes);
       R.fpend = false;
     }
     if constexpr ((DBG & 1) != 0) R.ppend = R.fpend = false;
     next_body();
     // A deferred traceback walk runs in the next body's columns (checked: rare).
     if (W.we && __builtin_amdgcn_ballot_w64(R.live) != 0) {
-      const uint32_t Pa = p_word(k1, a1, b1), Pb = p_word(k2, a2, b2);
-      if constexpr ((DBG & 1024) == 0) fetch(base + RT::chunk, a1, b1, a2, b2);
+      uint32_t Pw[kPw];
+      pwords(Pw, base);
       pk.ring = ring_block + slot * kSlotBytes;
-      if (W.we == 3) pk.template body<true, 3>(M0, M1, Pa, Pb, tr0, s_next, cols24);
-      else pk.template body<true, 2>(M0, M1, Pa, Pb, tr0, s_next, cols24);
+      if (W.we == 3) pk.template body<true, 3>(M, Pw, tr0, s_next, cols24);
+      else pk.template body<true, 2>(M, Pw, tr0, s_next, cols24);
       W.we = 0;
       if ((DBG & 1) == 0 && __builtin_amdgcn_ballot_w64(R.fpend) != 0) {   // (a partial window is 256 columns on)
-        traceback<Packet<CR, DBG>::V5>(R.fpend, R.fM0, R.fM1, R.fT, R.fcnt, R.flook, l, rib, ring_block, out, ooff,
-                                       R.nbytes);
+        traceback(R.fpend, R.fM, R.fT, R.fcnt, R.flook, l, rib, ring_block, out, ooff, R.nbytes);
         R.fpend = false;
       }
       if constexpr ((DBG & 1) != 0) R.ppend = R.fpend = false;
@@ -890,8 +933,8 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
                                              uint2* __restrict__ dumps, int32_t* __restrict__ stats) {
   constexpr int fix = FIX;
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t l = lane & 15u;
-  const uint32_t rib = threadIdx.x >> 4;               // row in block
+  const uint32_t l = lane & (v3::kLanes - 1u);
+  const uint32_t rib = threadIdx.x >> v3::kLaneBits;   // row in block
 #ifdef ZRX_VTRACE
   const uint32_t vt0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
@@ -902,7 +945,7 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
     uint32_t k = 0, nseg = 1;
     if (valid && rows) {
       if (uni) {                                       // a uniform batch: row r = segment r mod u of packet r / u
-        const uint32_t r = v3::order_place((uint32_t)slot, (uint32_t)nrows >> 4, ncu, ncu_rcp);
+        const uint32_t r = v3::order_place((uint32_t)slot, (uint32_t)nrows / v3::kRows, ncu, ncu_rcp);
         p = (int)v3::udiv_small(r, uni); k = r - (uint32_t)p * uni; nseg = uni;
       } else {
         const int2 r = rows[slot];
@@ -941,13 +984,10 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
       // state it reproduces (every segment after that one then starts right).
       uint32_t ks = 0, kl = 0;
       for (uint32_t jj = 1; __builtin_amdgcn_ballot_w64(work && jj < nseg) != 0; jj++) {
-        bool ne = false;
-        if (work && jj < nseg) {
-          const uint2 a = dumps[v3::seam_index((uint32_t)p, jj, 0) + l], b = dumps[v3::seam_index((uint32_t)p, jj, 1) + l];
-          ne = (((a.x ^ b.x) | (a.y ^ b.y)) & 0xFE00FE00u) != 0u;
-        }
+        const bool ne = work && jj < nseg &&
+                        v3::dump_ne(dumps + v3::seam_index((uint32_t)p, jj, 0), dumps + v3::seam_index((uint32_t)p, jj, 1), l);
         const uint64_t bad = __builtin_amdgcn_ballot_w64(ne);
-        if (((bad >> (lane & 48u)) & 0xFFFFu) != 0u) {
+        if (v3::row_bits(bad) != 0u) {
           if (ks == 0u) ks = jj;
           kl = jj;
         }
@@ -986,26 +1026,26 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
       // rows further apart than that run one at a time (correct, 4x the time; only batches
       // with more than 4 GiB of soft values can get there).
       const int64_t lo_me = mine ? so : INT64_MAX, hi_me = mine ? so + (int64_t)nS : INT64_MIN;
-      const int64_t lo_w = min(min(v3::rl64(lo_me, 0), v3::rl64(lo_me, 16)), min(v3::rl64(lo_me, 32), v3::rl64(lo_me, 48)));
-      const int64_t hi_w = max(max(v3::rl64(hi_me, 0), v3::rl64(hi_me, 16)), max(v3::rl64(hi_me, 32), v3::rl64(hi_me, 48)));
-      const int passes = hi_w - lo_w > v3::kSoftWindow ? 4 : 1;
+      const int64_t lo_w = v3::wave_min_rows64(lo_me);
+      const int64_t hi_w = v3::wave_max_rows64(hi_me);
+      const int passes = hi_w - lo_w > v3::kSoftWindow ? v3::kRowsWave : 1;
       for (int q = 0; q < passes; q++) {
-        const bool mq = mine && (passes == 1 || (int)(rib & 3u) == q);
+        const bool mq = mine && (passes == 1 || (int)(rib % v3::kRowsWave) == q);
         if (__builtin_amdgcn_ballot_w64(mq) == 0) continue;
         // start state, output base and first seam event of the row (v3::seg_start)
         const v3::RowX x = rowx[rib];
         const uint32_t xk = x.kn & 0xFFu, xn = (x.kn >> 8) & 0xFFu, xj = x.kn >> 20;
         const bool xfix = (x.kn >> 16) & 1u;
-        uint32_t M0, M1;
+        uint32_t M[v3::kDw];
         if (xfix && mq) {                               // segment ks - 1's exact state at S = C_ks
-          const uint2 a = dumps[v3::seam_index(x.p, x.kn & 0xFFu, 0) + l];
-          M0 = a.x; M1 = a.y;
+          v3::dump_load(dumps + v3::seam_index(x.p, x.kn & 0xFFu, 0), l, M);
         } else if (xk) {                                // warm-up from zero
-          M0 = M1 = 0u;
+#pragma unroll
+          for (int d = 0; d < v3::kDw; d++) M[d] = 0u;
         } else {                                        // ALL_INIT0 (viterbilut.h:74-82)
-          const uint32_t p0 = v3::pos_of(l, 0, 0), p1 = v3::pos_of(l, 0, 1), p2 = v3::pos_of(l, 1, 0), p3 = v3::pos_of(l, 1, 1);
-          M0 = ((p1 ? 48u : 0u) << 24) | ((p0 ? 48u : 0u) << 8);
-          M1 = ((p3 ? 48u : 0u) << 24) | ((p2 ? 48u : 0u) << 8);
+#pragma unroll
+          for (int d = 0; d < v3::kDw; d++)
+            M[d] = ((v3::pos_of(l, d, 1) ? 48u : 0u) << 24) | ((v3::pos_of(l, d, 0) ? 48u : 0u) << 8);
         }
         v3::Row Rr;
         Rr.ob = xfix ? v3::kSegWarm - v3::kSegCmp : xk ? v3::kSegWarm : 0u;
@@ -1014,12 +1054,13 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
         Rr.live = mq;
         Rr.ppend = Rr.fpend = false;
         Rr.pT = Rr.plook = Rr.fT = Rr.fcnt = Rr.flook = 0;
-        Rr.pM0 = Rr.pM1 = Rr.fM0 = Rr.fM1 = 0;
+#pragma unroll
+        for (int d = 0; d < v3::kDw; d++) Rr.pM[d] = Rr.fM[d] = 0u;
         Rr.nbytes = 0;
         Rr.next = v3::row_next(Rr);
-        if (rate == 0) v3::run_rows<0, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M0, M1, rowx, dumps);
-        else if (rate == 1) v3::run_rows<1, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M0, M1, rowx, dumps);
-        else v3::run_rows<2, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M0, M1, rowx, dumps);
+        if (rate == 0) v3::run_rows<0, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M, rowx, dumps);
+        else if (rate == 1) v3::run_rows<1, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M, rowx, dumps);
+        else v3::run_rows<2, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M, rowx, dumps);
         if (mq) nbytes = Rr.nbytes;
       }
     }
@@ -1043,7 +1084,7 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
   }
 }
 template <int DBG, bool FIX = false>
-__global__ __launch_bounds__(256, 4) void k_viterbi3(const uint8_t* __restrict__ soft, const int64_t* __restrict__ soft_off,
+__global__ __launch_bounds__(256, v3::kWavesPerSimd) void k_viterbi3(const uint8_t* __restrict__ soft, const int64_t* __restrict__ soft_off,
                                                   const int32_t* __restrict__ vparams, int nslots,
                                                   uint8_t* __restrict__ out, const int64_t* __restrict__ out_off,
                                                   int32_t* __restrict__ out_bits, const int2* __restrict__ rows,
@@ -1059,7 +1100,7 @@ __global__ __launch_bounds__(256, 4) void k_viterbi3(const uint8_t* __restrict__
   const uint32_t ncu_rcp = 0xFFFFFFFFu / ncu + 1u;
   if (FIX && uni == 1u) return;                        // a uniform batch of whole frames has no seams
   v3::Consts K;
-  v3::make_consts(K, threadIdx.x & 15u, threadIdx.x >> 4);
+  v3::make_consts(K, threadIdx.x & (v3::kLanes - 1u), threadIdx.x >> v3::kLaneBits);
   if constexpr (FIX) {                                 // block-stride over the packets
     for (int g0 = blockIdx.x * v3::kRows; g0 < nrows; g0 += gridDim.x * v3::kRows)
       viterbi_rows<DBG, true>(g0, nrows, uni, ncu, ncu_rcp, K, ring, rowx, soft, soft_off, vparams, out, out_off, out_bits, rows, segs, dumps,
@@ -1141,3 +1182,7 @@ __device__ __forceinline__ uint32_t order_hist_scan(uint32_t* hist) {
 }
 
 }  // namespace zrx
+
+
+
+
