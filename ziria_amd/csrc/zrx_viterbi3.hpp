@@ -688,13 +688,20 @@ struct Packet {
       walk_stepk(*W, (uint32_t)(J + 12), (uint32_t)NL, ring0, rib * 64u);
     }
   }
-  template <uint32_t O>
+  // ZRX_SNAP 0: byte stores by asm with a memory clobber; 1: without it (the body end is a
+// compiler barrier); 2: plain C++ byte stores (the compiler picks the instructions)
+#ifndef ZRX_SNAP
+#define ZRX_SNAP 0
+#endif
+template <uint32_t O>
 static __device__ __forceinline__ void ds_b8(uint32_t a, uint32_t v) {
-  asm volatile("ds_write_b8 %0, %1 offset:%2" ::"v"(a), "v"(v), "i"(O) : "memory");
+  if constexpr (ZRX_SNAP == 0) asm volatile("ds_write_b8 %0, %1 offset:%2" ::"v"(a), "v"(v), "i"(O) : "memory");
+  else asm volatile("ds_write_b8 %0, %1 offset:%2" ::"v"(a), "v"(v), "i"(O));
 }
 template <uint32_t O>
 static __device__ __forceinline__ void ds_b8_hi(uint32_t a, uint32_t v) {
-  asm volatile("ds_write_b8_d16_hi %0, %1 offset:%2" ::"v"(a), "v"(v), "i"(O) : "memory");
+  if constexpr (ZRX_SNAP == 0) asm volatile("ds_write_b8_d16_hi %0, %1 offset:%2" ::"v"(a), "v"(v), "i"(O) : "memory");
+  else asm volatile("ds_write_b8_d16_hi %0, %1 offset:%2" ::"v"(a), "v"(v), "i"(O));
 }
 // Snapshot k (column C = 8k + 6 of the body, C mod 6 = 2k): every position's pad byte
   // (bits 8..1 of its half) to the ring at the lane's first offset plus a lane-uniform delta.
@@ -712,9 +719,15 @@ static __device__ __forceinline__ void ds_b8_hi(uint32_t a, uint32_t v) {
     } else {
       // one address register serves all stores through their offsets: half 0 by
       // ds_write_b8, half 1 by ds_write_b8_d16_hi
-      const uint32_t a = lds_addr(s) + K.sa[k];
-      (ds_b8<snap_delta(k, D, 0)>(a, u[D]), ...);
-      (ds_b8_hi<snap_delta(k, D, 1)>(a, u[D]), ...);
+      if constexpr (ZRX_SNAP == 2) {
+        uint8_t* b = s + K.sa[k];
+        ((b[snap_delta(k, D, 0)] = (uint8_t)u[D]), ...);
+        ((b[snap_delta(k, D, 1)] = (uint8_t)(u[D] >> 16)), ...);
+      } else {
+        const uint32_t a = lds_addr(s) + K.sa[k];
+        (ds_b8<snap_delta(k, D, 0)>(a, u[D]), ...);
+        (ds_b8_hi<snap_delta(k, D, 1)>(a, u[D]), ...);
+      }
     }
   }
   template <int J, bool CHECKED, int WE>
@@ -755,6 +768,7 @@ static __device__ __forceinline__ void ds_b8_hi(uint32_t a, uint32_t v) {
       Pq[0] = bcast<0>(Pw); Pq[1] = bcast<1>(Pw); Pq[2] = bcast<2>(Pw); Pq[3] = bcast<3>(Pw);
     }
     (col<J, CHECKED, WE>(M, Pq, Pw, tr0, s_next), ...);
+    if constexpr (ZRX_SNAP != 0) asm volatile("" ::: "memory");   // the snapshot stores stay inside their body
   }
 };
 
@@ -940,7 +954,7 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
 #endif
   {
     const int slot = g0 + (int)rib;
-    const bool valid = slot < nrows;
+    bool valid = slot < nrows;
     int p = slot;
     uint32_t k = 0, nseg = 1;
     if (valid && rows) {
@@ -950,6 +964,7 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
       } else {
         const int2 r = rows[slot];
         p = r.x; k = (uint32_t)r.y & 0xFFu; nseg = ((uint32_t)r.y >> 8) & 0xFFu;
+        if (p < 0) { valid = false; p = 0; nseg = 1; k = 0; }   // a slot the wave placement left empty
       }
     }
 #ifdef ZRX_GUARD
