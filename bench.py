@@ -642,8 +642,8 @@ def cpu_baseline(b, seconds, chan=None):
     """The chain on every host core this process is allowed (host_cpus), packet-parallel with
     pthreads, over chunks of the same packets until `seconds` of wall time have passed: the
     fast CPU port (oracle/cpu_port.c: table FFT, AVX-512 Viterbi, table CRC; bit-identical to
-    the oracle, tests/test_cpu_port.py) for the time-domain chain, the scalar oracle for the
-    EQ chain (the port has no channel estimator)."""
+    the oracle, tests/test_cpu_port.py), with ChannelEqualization + PilotTrack for the EQ
+    chain."""
     from oracle import oracle as O
     threads, host = host_cpus()
     sym = b["sym"].cpu().numpy()
@@ -659,14 +659,15 @@ def cpu_baseline(b, seconds, chan=None):
         if ch_all is None:
             _, res = O.rx_batch_time_fast(sym, off_all[lo:hi], ns_all[lo:hi], nthreads=threads)
         else:
-            _, res = O.rx_batch_time_eq(sym, off_all[lo:hi], ns_all[lo:hi], ch_all[lo:hi], nthreads=threads)
+            _, res = O.rx_batch_time_eq_fast(sym, off_all[lo:hi], ns_all[lo:hi], ch_all[lo:hi], nthreads=threads)
         ok += sum(r["crc_ok"] for r in res)
         bits += sum((r["len"] - 4) * 8 for r in res if r["crc_ok"])
         done += hi - lo
     dt = time.perf_counter() - t0
-    what = ("scalar C oracle, EQ chain" if ch_all is not None else
-            "CPU port: table FFT, %s Viterbi, table CRC" %
-            ("AVX-512 vpermb" if getattr(O.rx_batch_time_fast, "avx512", False) else "scalar"))
+    fast = O.rx_batch_time_eq_fast if ch_all is not None else O.rx_batch_time_fast
+    what = "CPU port: table FFT, %s%s Viterbi, table CRC" % (
+        "the oracle's ChannelEqualization + PilotTrack, " if ch_all is not None else "",
+        "AVX-512 vpermb" if getattr(fast, "avx512", False) else "scalar")
     return {"value": round(bits / dt / 1e6, 2), "unit": "Mbit/s", "cores": threads, "kind": "port",
             "per_core": round(bits / dt / 1e6 / threads, 2), "host": host,
             "sample": f"{done} packets of the same batch ({ok} CRC-ok), {dt:.1f} s wall on {threads} threads "

@@ -323,12 +323,26 @@ static int have_avx512(void) {
 }
 static int g_avx;
 
-static void rx_packet(const zo_c16* sym, int nsym, uint8_t* payload, zo_rx_result* r, pv_t* v, zo_vit* zv) {
+/* FFT of symbol k of a packet; with chan64 (the EQ chain, receiver.blk:66-69) followed by
+   ChannelEqualization and PilotTrack (the oracle's restatements, ziria_oracle_eq.c) */
+static inline void fft_sym(const zo_c16* in, int k, const zo_c16* chan64, zo_c16* f) {
+  if (!chan64) {
+    if (g_avx) fft64_avx512(in, f); else fft64_fast(in, f);
+    return;
+  }
+  zo_c16 t[64], e[64];
+  if (g_avx) fft64_avx512(in, t); else fft64_fast(in, t);
+  zo_channel_eq(t, chan64, e);
+  zo_pilot_track(e, k, f);
+}
+
+static void rx_packet(const zo_c16* sym, int nsym, const zo_c16* chan64, uint8_t* payload, zo_rx_result* r, pv_t* v,
+                      zo_vit* zv) {
   memset(r, 0, sizeof(*r));
   if (nsym < 1) return;
   zo_c16 f[64], sub[48], lim[48];
   int8_t soft[288], di[288];
-  if (g_avx) fft64_avx512(sym, f); else fft64_fast(sym, f);   /* SIGNAL: DecodePLCP.blk:30-37 */
+  fft_sym(sym, 0, chan64, f);                          /* SIGNAL: DecodePLCP.blk:30-37 */
   zo_get_data(f, sub);
   zo_demap_limit(sub, 48, lim);
   zo_demap(0, lim, soft);
@@ -349,7 +363,7 @@ static void rx_packet(const zo_c16* sym, int nsym, uint8_t* payload, zo_rx_resul
     zo_vit_init(zv, len + 2, cod, 256);
   }
   for (int k = 0; k < nsym - 1 && bits < (len + 2) * 8; k++) {
-    if (g_avx) fft64_avx512(sym + 64 * (1 + k), f); else fft64_fast(sym + 64 * (1 + k), f);
+    fft_sym(sym + 64 * (1 + k), 1 + k, chan64, f);
     symbol_soft(f, mod, di);
     for (int c = 0; c < nc; c += 48)
       bits += g_avx ? pv_decode_avx512(v, di + c, 48, dec + bits / 8) : zo_vit_decode(zv, di + c, 48, dec + bits / 8);
@@ -365,6 +379,7 @@ typedef struct {
   const zo_c16* sym; const int64_t* off; const int32_t* n;
   uint8_t* out; int stride; zo_rx_result* res; int npkts;
   int* next;                                           /* shared packet counter (dynamic claim) */
+  const zo_c16* chan;                                  /* EQ chain: 64 coefficients per packet, else null */
 } pjob_t;
 static void* pworker(void* p) {
   pjob_t* j = (pjob_t*)p;
@@ -373,7 +388,8 @@ static void* pworker(void* p) {
   v.surv = (uint64_t*)calloc(v.cap, sizeof(uint64_t));
   zo_vit zv; memset(&zv, 0, sizeof(zv));
   for (int i; (i = __atomic_fetch_add(j->next, 1, __ATOMIC_RELAXED)) < j->npkts;)
-    rx_packet(j->sym + 64 * j->off[i], j->n[i], j->out + (size_t)i * j->stride, &j->res[i], &v, &zv);
+    rx_packet(j->sym + 64 * j->off[i], j->n[i], j->chan ? j->chan + 64 * (size_t)i : 0, j->out + (size_t)i * j->stride,
+              &j->res[i], &v, &zv);
   free(v.surv);
   zo_vit_free(&zv);
   return 0;
@@ -433,9 +449,8 @@ int zp_fft64(const zo_c16* in, zo_c16* out, int n) {
   return g_avx;
 }
 
-/* Same contract as zo_rx_batch_time.  Returns 1 when the AVX-512 ACS ran, 0 otherwise. */
-int zp_rx_batch_time(const zo_c16* sym, const int64_t* sym_off, const int32_t* nsym, int npkts,
-                     uint8_t* payload, int payload_stride, zo_rx_result* res, int nthreads) {
+static int rx_batch(const zo_c16* sym, const int64_t* sym_off, const int32_t* nsym, int npkts, const zo_c16* chan,
+                    uint8_t* payload, int payload_stride, zo_rx_result* res, int nthreads) {
   pthread_once(&g_once, init_all);
   if (nthreads < 1) nthreads = 1;
   if (nthreads > 256) nthreads = 256;
@@ -443,11 +458,22 @@ int zp_rx_batch_time(const zo_c16* sym, const int64_t* sym_off, const int32_t* n
   pjob_t jobs[256];
   int next = 0;
   for (int t = 0; t < nthreads; t++) {
-    pjob_t j = {sym, sym_off, nsym, payload, payload_stride, res, npkts, &next};
+    pjob_t j = {sym, sym_off, nsym, payload, payload_stride, res, npkts, &next, chan};
     jobs[t] = j;
   }
   for (int t = 1; t < nthreads; t++) pthread_create(&th[t], 0, pworker, &jobs[t]);
   pworker(&jobs[0]);
   for (int t = 1; t < nthreads; t++) pthread_join(th[t], 0);
   return g_avx;
+}
+
+/* Same contract as zo_rx_batch_time.  Returns 1 when the AVX-512 ACS ran, 0 otherwise. */
+int zp_rx_batch_time(const zo_c16* sym, const int64_t* sym_off, const int32_t* nsym, int npkts,
+                     uint8_t* payload, int payload_stride, zo_rx_result* res, int nthreads) {
+  return rx_batch(sym, sym_off, nsym, npkts, 0, payload, payload_stride, res, nthreads);
+}
+/* Same contract as zo_rx_batch_time_eq (FFT >>> ChannelEqualization >>> PilotTrack >>> ...). */
+int zp_rx_batch_time_eq(const zo_c16* sym, const int64_t* sym_off, const int32_t* nsym, int npkts, const zo_c16* chan,
+                        uint8_t* payload, int payload_stride, zo_rx_result* res, int nthreads) {
+  return rx_batch(sym, sym_off, nsym, npkts, chan, payload, payload_stride, res, nthreads);
 }

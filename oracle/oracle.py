@@ -382,6 +382,24 @@ def rx_batch_time_eq(sym, sym_off, nsym, chan, payload_stride=4096, nthreads=1):
 
 
 
+def rx_batch_time_eq_fast(sym, sym_off, nsym, chan, payload_stride=4096, nthreads=1):
+    """rx_batch_time_eq by the fast CPU port (cpu_port.c: its FFT and Viterbi around the
+    oracle's ChannelEqualization / PilotTrack), bit-identical (tests/test_cpu_port.py);
+    bench.py --eq's cpu_baseline leg."""
+    sym = np.ascontiguousarray(sym, np.int16)
+    sym_off = np.ascontiguousarray(sym_off, np.int64)
+    nsym = np.ascontiguousarray(nsym, np.int32)
+    chan = np.ascontiguousarray(chan, np.int16)
+    n = sym_off.size
+    pay = np.zeros((n, payload_stride), np.uint8)
+    res = (RxResult * n)()
+    L = lib()
+    L.zp_rx_batch_time_eq.restype = C.c_int
+    rx_batch_time_eq_fast.avx512 = bool(L.zp_rx_batch_time_eq(_p(sym), _p(sym_off), _p(nsym), n, _p(chan), _p(pay),
+                                                              payload_stride, res, nthreads))
+    return pay, [_res(r) for r in res]
+
+
 # ---------------------------------------------------------------- RX front end
 class CCA(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("noSamples", "shift", "energy", "noise", "maxCorr")]

@@ -84,6 +84,8 @@ int zp_viterbi_batch(const int8_t* soft, const int64_t* soft_off, const int32_t*
                      uint8_t* out, const int64_t* out_off, int nthreads);
 int zp_rx_batch_time(const zo_c16* sym, const int64_t* sym_off, const int32_t* nsym, int npkts,
                      uint8_t* payload, int payload_stride, zo_rx_result* res, int nthreads);
+int zp_rx_batch_time_eq(const zo_c16* sym, const int64_t* sym_off, const int32_t* nsym, int npkts, const zo_c16* chan,
+                        uint8_t* payload, int payload_stride, zo_rx_result* res, int nthreads);
 /* same, fed frequency-domain data subcarriers (48 per symbol, GetData order) */
 int zo_rx_packet_freq(const zo_c16* sub48, int nsym, uint8_t* payload, zo_rx_result* r);
 

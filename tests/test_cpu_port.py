@@ -72,3 +72,21 @@ def test_port_viterbi_batch_vs_oracle(oracle):
     a = oracle.viterbi_batch(*args, nthreads=4)
     b = oracle.viterbi_batch(*args, nthreads=4, fast=True)
     assert (a == b).all()
+
+
+def test_port_eq_chain_vs_oracle(oracle, golden):
+    """the port's EQ chain (bench.py --eq cpu_baseline) equals the oracle's: the reference
+    fixture's packets and a synthetic channel batch at two noise levels"""
+    eq = golden["ref_eq"]
+    args = (eq["eq_sym"], eq["eq_off"], eq["eq_nsym"], eq["eq_chan"])
+    p1, r1 = oracle.rx_batch_time_eq(*args, nthreads=4)
+    p2, r2 = oracle.rx_batch_time_eq_fast(*args, nthreads=4)
+    assert r1 == r2 and (p1 == p2).all()
+    for seed, sigma in ((5, 2.0), (6, 40.0)):
+        b = txgen.make_batch(64, seed=seed, sigma=sigma, channel=True)
+        a = (b["sym"].numpy(), b["sym_off"].numpy(), b["nsym"].numpy(), b["chan"].numpy())
+        p1, r1 = oracle.rx_batch_time_eq(*a, nthreads=8)
+        p2, r2 = oracle.rx_batch_time_eq_fast(*a, nthreads=8)
+        assert r1 == r2 and (p1 == p2).all()
+        if sigma < 10:
+            assert sum(x["crc_ok"] for x in r2) > 32
