@@ -83,22 +83,3 @@ def test_pure_noise_many_seams(oracle):
         s = synth.viterbi_soft(2, 2035, -1, seed=seed)
         got, _ = SM.segmented_decode(s, 2, 2035, 8)
         assert (got == oracle.viterbi_decode(s, 2035, 2)).all(), seed
-
-
-def _block_place(rank, nb, ncu):
-    """restates zrx_kernels.hip block_place: block rank -> block index"""
-    q, c = divmod(rank, ncu)
-    m = min(ncu, nb - q * ncu)
-    return q * ncu + (m - 1 - c if q & 1 else c)
-
-
-def test_block_place_snake():
-    """the mixed plan's block placement is a bijection onto [0, nb), and in whole rounds the
-    CU given one round's k-th longest block gets the next round's k-th shortest"""
-    ncu = 256
-    for nb in (1, 100, ncu, ncu + 7, 2 * ncu - 3, 2 * ncu, 3 * ncu + 11):
-        blocks = [_block_place(r, nb, ncu) for r in range(nb)]
-        assert sorted(blocks) == list(range(nb))
-        if nb >= 2 * ncu:
-            for k in range(ncu):
-                assert blocks[k] % ncu == blocks[2 * ncu - 1 - k] % ncu

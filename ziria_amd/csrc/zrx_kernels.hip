@@ -284,35 +284,30 @@ __device__ __forceinline__ void plan_pkts(const int32_t* __restrict__ vparams, i
     if ((t & 63) == 0) atomicAdd(nrows_total, my_rows);
   }
 }
-// A mixed batch's row blocks (kRows consecutive rows of the (rate, length) order, so the
-// four waves of a block are alike) ranked by length, longest first, are placed snake over
-// the CUs: block rank r of round q = r / ncu goes to CU c = r mod ncu (reversed in odd
-// rounds) as block q ncu + c, the block the dispatcher puts on CU c (scripts/ubench/hwid.hip),
-// so the CU holding one of the longest blocks of one round gets one of the shortest of the
-// next beside it.  (v3::order_place does the same over the (rate, length) order, in which the
-// rates' length runs follow each other.)  At most kBlockRankMax blocks (LDS keys); a batch
-// with more keeps v3::order_place.
-constexpr int kBlockRankMax = 4096;
-#ifndef ZRX_BLOCK_RANK
-#define ZRX_BLOCK_RANK 0       // (1: rank row blocks by length; under A/B)
-#endif
-// (a partial last round of m < ncu blocks is reversed within its m: a bijection onto [0, nb))
-__device__ __forceinline__ uint32_t block_place(uint32_t rank, uint32_t nb, uint32_t ncu) {
-  const uint32_t q = rank / ncu;
-  const uint32_t c = rank - q * ncu, m = min(ncu, nb - q * ncu);
-  return q * ncu + ((q & 1u) ? m - 1u - c : c);
-}
-// Expand: the segments of the packet at sorted position i are rows prefix(i) .. +nseg - 1
-// (consecutive, so a wave holds segments of one or two packets of similar length).  Thread t
-// takes positions 16t .. 16t + 15 of each round.  PH 0: each block's length key (its first
-// row's segment length, in 24-column bodies, longest = 0) into bkey[]; PH 1: the rows, placed
-// by block rank (bkey[] holds the ranks then) or by v3::order_place (bkey null).
-template <int PH>
-__device__ __forceinline__ void plan_expand(const int32_t* __restrict__ vparams, uint32_t npk, int2* __restrict__ rows,
-                                            const uint8_t* __restrict__ segs, const int32_t* __restrict__ order,
-                                            uint32_t total, uint32_t ncu2, int rows_cap, uint32_t* bkey) {
+// The mixed batch's rows (k_pkt_plan's comment): packets keyed by (rate, segment length)
+// with segment length Lm, counted and scattered in LDS (hist: kOrderPerThread x 1024 words,
+// zeroed; *rtotal zeroed), then expanded onto rows by a block scan.  1024 threads.
+// (Tried: row blocks re-ranked by length across the rates before the snake placement;
+// config 5's Viterbi 0.672 -> 0.75 ms.)
+__device__ __forceinline__ void plan_rows_mixed(const int32_t* __restrict__ vparams, int npkts, uint32_t Lm,
+                                                int2* __restrict__ rows, int32_t* __restrict__ nrows,
+                                                uint8_t* __restrict__ segs, int32_t* __restrict__ order,
+                                                int32_t* __restrict__ out_bits, int ncu, int rows_cap, uint32_t* hist,
+                                                uint32_t* rtotal) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const uint32_t nfull = total / (uint32_t)v3::kRows, ncu_rcp = 0xFFFFFFFFu / ncu2 + 1u;
+  plan_pkts<false>(vparams, npkts, Lm, hist, order, segs, out_bits, rtotal);
+  __syncthreads();
+  if (ZRX_PLAN_CUT <= 3) return;
+  const uint32_t npk = order_hist_scan(hist);          // packets with rows
+  __syncthreads();
+  plan_pkts<true>(vparams, npkts, Lm, hist, order, segs, out_bits, nullptr);
+  __syncthreads();                                     // order[] and segs[] written by the block
+  if (ZRX_PLAN_CUT <= 5) return;
+  // Expand: the segments of the packet at sorted position i are rows prefix(i) .. +nseg - 1
+  // (consecutive, so a wave holds segments of one or two packets of similar length), placed
+  // snake over the CUs.  Thread t takes positions 16t .. 16t + 15 of each round.
+  const uint32_t total = *rtotal, nfull = total / (uint32_t)v3::kRows;
+  const uint32_t ncu2 = (uint32_t)max(ncu, 2), ncu_rcp = 0xFFFFFFFFu / ncu2 + 1u;
   __shared__ uint32_t esum[16];
   uint32_t carry = 0;
   for (uint32_t base = 0; base < npk; base += 1024u * kScanPer) {
@@ -332,71 +327,17 @@ __device__ __forceinline__ void plan_expand(const int32_t* __restrict__ vparams,
     for (int w = 0; w < 16; w++) { ex += w < wv ? esum[w] : 0u; rnd += esum[w]; }
 #pragma unroll
     for (int i = 0; i < kScanPer; i++) {
-      if constexpr (PH == 0) {
-        if (ns[i] && ((ex + ns[i] - 1u) / (uint32_t)v3::kRows != (ex - 1u) / (uint32_t)v3::kRows || ex == 0u)) {
-          // a block starts at one of this packet's rows: key = its segment length (plan_pkts)
-          const int4 q = *reinterpret_cast<const int4*>(vparams + 4 * (int64_t)pk[i]);
-          const uint32_t cols = cols_of(q.y, q.z);
-          const uint32_t len = ns[i] <= 1u ? cols : v3::udiv_small(min(cols, (1u << 20) - 1u) + ns[i] - 1u, ns[i]) + 286u;
-          const uint32_t key = (uint32_t)kOrderLen - 1u - min((len + 23u) / 24u, (uint32_t)kOrderLen - 1u);
-          for (uint32_t k = 0; k < ns[i]; k++)
-            if ((ex + k) % (uint32_t)v3::kRows == 0u) bkey[(ex + k) / (uint32_t)v3::kRows] = key;
-        }
-      } else {
-        for (uint32_t k = 0; k < ns[i]; k++) {
-          const uint32_t pos = ex + k;
-          const uint32_t at = bkey ? block_place(bkey[pos / (uint32_t)v3::kRows], (total + v3::kRows - 1u) / (uint32_t)v3::kRows, ncu2) * (uint32_t)v3::kRows +
-                                         pos % (uint32_t)v3::kRows
-                                   : v3::order_place(pos, nfull, ncu2, ncu_rcp);
-          if (at < (uint32_t)rows_cap) rows[at] = make_int2(pk[i], (int)(k | (ns[i] << 8)));   // (always: the plan's row bound)
-        }
+      for (uint32_t k = 0; k < ns[i]; k++) {
+        const uint32_t at = v3::order_place(ex + k, nfull, ncu2, ncu_rcp);
+        if (at < (uint32_t)rows_cap) rows[at] = make_int2(pk[i], (int)(k | (ns[i] << 8)));   // (always: the plan's row bound)
       }
       ex += ns[i];
     }
     carry += rnd;
     __syncthreads();                                   // esum is rewritten by the next round
   }
-}
-// The mixed batch's rows (k_pkt_plan's comment): packets keyed by (rate, segment length)
-// with segment length Lm, counted and scattered in LDS (hist: kOrderPerThread x 1024 words,
-// zeroed; *rtotal zeroed), expanded onto rows by a block scan, row blocks ranked by length
-// and placed snake over the CUs (block_place).  1024 threads.
-__device__ __forceinline__ void plan_rows_mixed(const int32_t* __restrict__ vparams, int npkts, uint32_t Lm,
-                                                int2* __restrict__ rows, int32_t* __restrict__ nrows,
-                                                uint8_t* __restrict__ segs, int32_t* __restrict__ order,
-                                                int32_t* __restrict__ out_bits, int ncu, int rows_cap, uint32_t* hist,
-                                                uint32_t* rtotal) {
-  const int t = threadIdx.x;
-  plan_pkts<false>(vparams, npkts, Lm, hist, order, segs, out_bits, rtotal);
-  __syncthreads();
-  if (ZRX_PLAN_CUT <= 3) return;
-  const uint32_t npk = order_hist_scan(hist);          // packets with rows
-  __syncthreads();
-  plan_pkts<true>(vparams, npkts, Lm, hist, order, segs, out_bits, nullptr);
-  __syncthreads();                                     // order[] and segs[] written by the block
-  if (ZRX_PLAN_CUT <= 5) return;
-  const uint32_t total = *rtotal;
-  const uint32_t ncu2 = (uint32_t)max(ncu, 2);
-  const uint32_t nb = (total + v3::kRows - 1u) / (uint32_t)v3::kRows;
-  __shared__ uint32_t bkey[kBlockRankMax];
-  const bool ranked = ZRX_BLOCK_RANK && nb <= (uint32_t)kBlockRankMax && nb * (uint32_t)v3::kRows <= (uint32_t)rows_cap;
-  if (ranked) {
-    plan_expand<0>(vparams, npk, rows, segs, order, total, ncu2, rows_cap, bkey);
-    for (int i = t; i < kOrderPerThread * 1024; i += 1024) hist[i] = 0;
-    __syncthreads();
-    for (uint32_t v = t; v < nb; v += 1024u) atomicAdd(&hist[bkey[v]], 1u);
-    __syncthreads();
-    order_hist_scan(hist);
-    __syncthreads();
-    for (uint32_t v = t; v < nb; v += 1024u) bkey[v] = atomicAdd(&hist[bkey[v]], 1u);   // key -> rank
-    __syncthreads();
-    // the last block's empty slots, wherever that block lands
-    for (uint32_t r = total + t; r < nb * (uint32_t)v3::kRows; r += 1024u)
-      rows[block_place(bkey[nb - 1u], nb, ncu2) * (uint32_t)v3::kRows + r % (uint32_t)v3::kRows] = make_int2(-1, 0);
-  }
-  plan_expand<1>(vparams, npk, rows, segs, order, total, ncu2, rows_cap, ranked ? bkey : nullptr);
   if (t == 0) {
-    nrows[v3::kPlanRows] = (int32_t)min(ranked ? nb * (uint32_t)v3::kRows : total, (uint32_t)rows_cap);
+    nrows[v3::kPlanRows] = (int32_t)min(total, (uint32_t)rows_cap);
     nrows[v3::kPlanFixes] = 0;                         // counted by the seam pass
     nrows[v3::kPlanUniform] = 0;
     // rows past the bound (plan_rows_max) are dropped: never by construction, but a wrong
