@@ -644,6 +644,12 @@ __device__ __forceinline__ PKind p_kind(uint32_t r) {
   return r == 0 ? PKind{0x0E0E0000u, 0xFFFFFFFFu, 0x0E000E00u}
                 : (r == 1 ? PKind{0x0E0E0000u, 0u, 0u} : PKind{0x0E000E00u, 0u, 0u});
 }
+// the same from bytes of an 8-byte pair {hi:lo}: selA / selB replicate byte a / b
+__device__ __forceinline__ uint32_t p_word_sel(const PKind& k, uint32_t hi, uint32_t lo, uint32_t selA, uint32_t selB) {
+  const uint32_t a2 = (__builtin_amdgcn_perm(hi, lo, selA) << 1) & 0x0E0E0E0Eu;
+  const uint32_t b2 = (__builtin_amdgcn_perm(hi, lo, selB) << 1) & (0x0E0E0E0Eu & k.Mb);
+  return (a2 ^ k.X) + (b2 ^ k.Y);
+}
 __device__ __forceinline__ uint32_t p_word(const PKind& k, uint32_t a, uint32_t b) {
   // v replicated into 4 bytes (v_perm), doubled and masked to 2(v & 7) in each byte
   const uint32_t a2 = (__builtin_amdgcn_perm(0u, a, 0u) << 1) & 0x0E0E0E0Eu;
@@ -656,10 +662,20 @@ __device__ __forceinline__ uint32_t p_word(const PKind& k, uint32_t a, uint32_t 
 // 64 ds_swizzle issued 4 columns ahead behind a scheduling barrier, 1024 no soft fetch
 // (every body reuses the first body's soft values).  All are timing-only (wrong output).
 constexpr int kPw = (24 + kLanes - 1) / kLanes;        // P words a lane builds per body (3 or 2)
+// 8-lane rows: lane l builds the P words of body columns 3l .. 3l + 2, whose soft values are
+// consecutive bytes, read as 2-3 dwords per body instead of 6 byte loads (ZRX_DWFETCH 0: the
+// byte loads, lane l building columns l, 8 + l, 16 + l)
+#ifndef ZRX_DWFETCH
+#define ZRX_DWFETCH 1
+#endif
+constexpr bool kDwFetch = kLanes == 8 && ZRX_DWFETCH != 0;
 #ifndef ZRX_VPF
 #define ZRX_VPF 1
 #endif
 constexpr int kPf = ZRX_VPF;                           // bodies the soft-value fetch runs ahead
+// P words are broadcast kPq columns ahead of their column.  (Queues of 8 and 24, and each
+// broadcast pinned where it is issued by a scheduling barrier, measured the same.)
+constexpr int kPq = 4;
 template <int CR, int DBG = 0>
 struct Packet {
   using RT = Rate<CR>;
@@ -675,7 +691,10 @@ struct Packet {
   // P word of body column J: lane J mod kLanes of the row built it as its word J / kLanes
   template <int J>
   static __device__ __forceinline__ uint32_t bcast(const uint32_t (&Pw)[kPw]) {
-    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)Pw[J / kLanes], ((J % kLanes) << 5) | (32 - kLanes));
+    if constexpr (kDwFetch)   // lane J / 3 built columns 3l .. 3l + 2
+      return (uint32_t)__builtin_amdgcn_ds_swizzle((int)Pw[J % 3], ((J / 3) << 5) | (32 - kLanes));
+    else
+      return (uint32_t)__builtin_amdgcn_ds_swizzle((int)Pw[J / kLanes], ((J % kLanes) << 5) | (32 - kLanes));
   }
   // The deferred traceback steps of column J (branch-free; see Walk): steps 2J, 2J + 1 in
   // columns 0..11, step J + 12 after, NL + 32 steps in all.
@@ -688,7 +707,11 @@ struct Packet {
       walk_stepk(*W, (uint32_t)(J + 12), (uint32_t)NL, ring0, rib * 64u);
     }
   }
-  // Snapshot k (column C = 8k + 6 of the body, C mod 6 = 2k): every position's pad byte
+  template <uint32_t O>
+static __device__ __forceinline__ void ds_b8_hi(uint32_t a, uint32_t v) {
+  asm volatile("ds_write_b8_d16_hi %0, %1 offset:%2" ::"v"(a), "v"(v), "i"(O));
+}
+// Snapshot k (column C = 8k + 6 of the body, C mod 6 = 2k): every position's pad byte
   // (bits 8..1 of its half) to the ring at the lane's first offset plus a lane-uniform delta.
   template <int k, int... D>
   __device__ __forceinline__ void snapshot(const uint32_t (&M)[kDw], std::integer_sequence<int, D...>) {
@@ -702,24 +725,27 @@ struct Packet {
       for (int e = 0; e < kDw / 2; e++)
         *(uint32_t*)(s + K.sa[2] + snap_delta(2, 2 * e, 0)) = __builtin_amdgcn_perm(u[2 * e + 1], u[2 * e], 0x06020400u);
     } else {
-      // plain byte stores at constant offsets from one address: the compiler emits
-      // ds_write_b8 / ds_write_b8_d16_hi and schedules them (asm stores with a memory
-      // clobber measured 0.7-1.5 % slower)
+      // byte stores at constant offsets from one address: half 0 by a plain store (the
+      // compiler emits and schedules ds_write_b8), half 1 by ds_write_b8_d16_hi (the
+      // compiler would shift first).  The asm has no memory clobber (one cost 0.7-1.5 %):
+      // nothing in the body reads a slot its snapshots write, and the tracebacks that do
+      // run after the body's branch.
       uint8_t* b = s + K.sa[k];
       ((b[snap_delta(k, D, 0)] = (uint8_t)u[D]), ...);
-      ((b[snap_delta(k, D, 1)] = (uint8_t)(u[D] >> 16)), ...);
+      const uint32_t a = lds_addr(s) + K.sa[k];
+      (ds_b8_hi<snap_delta(k, D, 1)>(a, u[D]), ...);
     }
   }
   template <int J, bool CHECKED, int WE>
-  __device__ __forceinline__ void col(uint32_t (&M)[kDw], uint32_t (&Pq)[4], const uint32_t (&Pw)[kPw],
+  __device__ __forceinline__ void col(uint32_t (&M)[kDw], uint32_t (&Pq)[kPq], const uint32_t (&Pw)[kPw],
                                       uint32_t tr0, uint32_t& s_next) {
     if constexpr (WE > 0) walk_col<J, WE>();
     uint32_t P;
     if constexpr ((DBG & 8) != 0) {
       P = Pw[J / kLanes];
     } else {
-      P = Pq[J & 3];
-      if constexpr (J + 4 < 24) Pq[J & 3] = bcast<J + 4>(Pw);   // issued 4 columns ahead
+      P = Pq[J % kPq];
+      if constexpr (J + kPq < 24) Pq[J % kPq] = bcast<J + kPq>(Pw);   // issued kPq columns ahead
       if constexpr ((DBG & 64) != 0) __builtin_amdgcn_sched_barrier(0);
     }
     constexpr int r = J % RT::steps;
@@ -740,13 +766,15 @@ struct Packet {
       }
     }
   }
+  template <int... Q>
+  static __device__ __forceinline__ void pq_fill(uint32_t (&Pq)[kPq], const uint32_t (&Pw)[kPw], std::integer_sequence<int, Q...>) {
+    ((Pq[Q] = bcast<Q>(Pw)), ...);
+  }
   template <bool CHECKED, int WE, int... J>
   __device__ __forceinline__ void body(uint32_t (&M)[kDw], const uint32_t (&Pw)[kPw], uint32_t tr0, uint32_t& s_next,
                                        std::integer_sequence<int, J...>) {
-    uint32_t Pq[4] = {0, 0, 0, 0};
-    if constexpr (!(DBG & 8)) {
-      Pq[0] = bcast<0>(Pw); Pq[1] = bcast<1>(Pw); Pq[2] = bcast<2>(Pw); Pq[3] = bcast<3>(Pw);
-    }
+    uint32_t Pq[kPq];
+    if constexpr (!(DBG & 8)) pq_fill(Pq, Pw, std::make_integer_sequence<int, kPq>{});
     (col<J, CHECKED, WE>(M, Pq, Pw, tr0, s_next), ...);
   }
 };
@@ -787,56 +815,83 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
   Packet<CR, DBG> pk{K, R, l, rib, ring_block, ring_block, &W, rowx, dumps};
   // this lane builds the P words of body columns kLanes i + l (i < kPw; 16-lane rows: the
   // second word of lanes 8..15 repeats lanes 0..7's)
-  uint32_t vo[kPw];
-  PKind kd[kPw];
-#pragma unroll
-  for (int i = 0; i < kPw; i++) {
-    const uint32_t j = kLanes * i + ((kLanes * i + l < 24u) ? l : (l & 7u));
-    vo[i] = soft_off<CR>(j);
-    kd[i] = p_kind(j % RT::steps);
-  }
   // Soft values by buffer loads: one wave-uniform descriptor over the rows' soft windows,
   // advanced by the scalar unit every body, and a per-lane byte offset that never changes
-  // (row offset + column offset; b at offset:1).  Reads past the furthest row's last soft
-  // value fall outside the descriptor and return 0; reads past a row's own end read its
-  // neighbour's values, which feed only columns beyond R.cols.  The caller (k_viterbi3)
-  // passes rows whose soft values lie within kSoftWindow of each other.
+  // (row offset + column offset).  Reads past the furthest row's last soft value fall outside
+  // the descriptor and return 0; reads past a row's own end read its neighbour's values,
+  // which feed only columns beyond R.cols.  The caller (k_viterbi3) passes rows whose soft
+  // values lie within kSoftWindow of each other.
   const int64_t lo_me = R.live ? so : INT64_MAX, hi_me = R.live ? so + (int64_t)n : INT64_MIN;
-  const int64_t lo_w = wave_min_rows64(lo_me);
-  const int64_t hi_w = wave_max_rows64(hi_me);
+  const int64_t lo_w = wave_min_rows64(lo_me) & ~(int64_t)3;   // (dword-aligned: soft is)
+  const int64_t hi_w = (wave_max_rows64(hi_me) + 3) & ~(int64_t)3;
   if (hi_w - lo_w > kSoftWindow) {                     // one row's soft values beyond 4 GiB: not decodable
     if (R.live) R.nbytes = 0xFFFFFFFFu;
     return;
   }
   const uint32_t rel = R.live ? (uint32_t)(so - lo_w) : 0u;
+  PKind kd[kPw];
+  // kDwFetch: dwords dw0, +4, +8 hold this lane's bytes; word i's a / b are bytes sa_/sb_ of
+  // {D1:D0} (or {D2:D1} for word 2 at rate 1/2)
+  constexpr int nD = kDwFetch ? (CR == 0 ? 3 : 2) : 2 * kPw;
+  uint32_t vo[kDwFetch ? 1 : kPw], selA[kPw], selB[kPw];
+  if constexpr (kDwFetch) {
+    const uint32_t j0 = 3u * l, off0 = soft_off<CR>(j0);
+    const uint32_t w0 = rel + off0, sh = w0 & 3u;
+    vo[0] = w0 & ~3u;
 #pragma unroll
-  for (int i = 0; i < kPw; i++) vo[i] += rel;
-  // soft bytes of the next kPf bodies in flight (sa[0]: the next body's)
-  uint32_t sa[kPf][kPw], sb[kPf][kPw];
-  auto fetch_into = [&](uint32_t (&A)[kPw], uint32_t (&B)[kPw], uint32_t base) {
+    for (int i = 0; i < kPw; i++) {
+      kd[i] = p_kind((j0 + i) % RT::steps);
+      uint32_t q = soft_off<CR>(j0 + i) - off0 + sh;
+      if (CR == 0 && i == 2) q -= 4u;                  // from {D2:D1}
+      selA[i] = q * 0x01010101u;
+      selB[i] = (q + 1u) * 0x01010101u;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < kPw; i++) {
+      const uint32_t j = kLanes * i + ((kLanes * i + l < 24u) ? l : (l & 7u));
+      vo[i] = soft_off<CR>(j) + rel;
+      kd[i] = p_kind(j % RT::steps);
+    }
+  }
+  // soft words / bytes of the next kPf bodies in flight (sd[0]: the next body's)
+  uint32_t sd[kPf][nD];
+  auto fetch_into = [&](uint32_t (&D)[nD], uint32_t base) {
     const int64_t left = hi_w - lo_w - (int64_t)base;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(soft + lo_w + base), (short)0, (int)(uint32_t)(left > 0 ? left : 0), 0x00020000);
+    if constexpr (kDwFetch) {
 #pragma unroll
-    for (int i = 0; i < kPw; i++) {
-      A[i] = __builtin_amdgcn_raw_buffer_load_b8(rs, (int)vo[i], 0, 0);
-      B[i] = __builtin_amdgcn_raw_buffer_load_b8(rs, (int)vo[i] + 1, 0, 0);
+      for (int d = 0; d < nD; d++) D[d] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)vo[0] + 4 * d, 0, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < kPw; i++) {
+        D[2 * i] = __builtin_amdgcn_raw_buffer_load_b8(rs, (int)vo[i], 0, 0);
+        D[2 * i + 1] = __builtin_amdgcn_raw_buffer_load_b8(rs, (int)vo[i] + 1, 0, 0);
+      }
     }
   };
-  // P words of the body at `base` from sa[0], then the fetch window moves one body on
+  // P words of the body at `base` from sd[0], then the fetch window moves one body on
   auto pwords = [&](uint32_t (&Pw)[kPw], uint32_t base_) {
 #pragma unroll
-    for (int i = 0; i < kPw; i++) Pw[i] = p_word(kd[i], sa[0][i], sb[0][i]);
+    for (int i = 0; i < kPw; i++) {
+      if constexpr (kDwFetch) {
+        const uint32_t lo = (CR == 0 && i == 2) ? sd[0][1] : sd[0][0], hi = (CR == 0 && i == 2) ? sd[0][2] : sd[0][1];
+        Pw[i] = p_word_sel(kd[i], hi, lo, selA[i], selB[i]);
+      } else {
+        Pw[i] = p_word(kd[i], sd[0][2 * i], sd[0][2 * i + 1]);
+      }
+    }
     if constexpr ((DBG & 1024) == 0) {
 #pragma unroll
       for (int q = 0; q + 1 < kPf; q++)
 #pragma unroll
-        for (int i = 0; i < kPw; i++) { sa[q][i] = sa[q + 1][i]; sb[q][i] = sb[q + 1][i]; }
-      fetch_into(sa[kPf - 1], sb[kPf - 1], base_ + kPf * RT::chunk);   // (latency hidden behind kPf bodies)
+        for (int i = 0; i < nD; i++) sd[q][i] = sd[q + 1][i];
+      fetch_into(sd[kPf - 1], base_ + kPf * RT::chunk);   // (latency hidden behind kPf bodies)
     }
   };
 #pragma unroll
-  for (int q = 0; q < kPf; q++) fetch_into(sa[q], sb[q], q * RT::chunk);
+  for (int q = 0; q < kPf; q++) fetch_into(sd[q], q * RT::chunk);
   uint32_t s_next = wave_min_rows(R.next);
   uint32_t slot = 0;                                   // first slot of this body (3 per body)
   uint32_t tr0 = 0, base = 0;
