@@ -41,6 +41,8 @@ def trace(name, b):
     rows, fixes = eng.plan_stats()
     t = buf.view(-1, 8)[:rows].cpu().numpy().astype(np.int64)
     np.savez_compressed(f"gpurun_out/vtrace_{name}.npz", t=t, rows=rows, fixes=fixes)
+    t = t[t[:, 0] != 0]                                  # (slots a chained plan left empty)
+    rows = t.shape[0]
     t0 = t[:, 0] - t[:, 0].min()
     t1 = t[:, 1] - t[:, 0].min()
     hw, xcc = t[:, 2], t[:, 3]
@@ -63,9 +65,9 @@ def trace(name, b):
           f"waves per SIMD min {nw.min()} max {nw.max()}; columns per SIMD min {c.min()} mean {c.mean():.0f} "
           f"max {c.max()}; wave starts after 5 us: {int((t0 > 500).sum())} rows", flush=True)
     busy = np.zeros(int(span) // 10 + 1)
-    for i in range(0, rows, 4):
+    for i in range(0, rows, 8):
         busy[int(t0[i]) // 10:int(t1[i]) // 10 + 1] += 1
-    print("  waves running per 10 us (of 4096 slots):", " ".join(str(int(x)) for x in busy[::5]), flush=True)
+    print("  waves running per 10 us (of 2048 slots):", " ".join(str(int(x)) for x in busy[::5][:400]), flush=True)
 
 
 trace("c5", txgen.make_mixed_fast(16384, min_len=64, max_len=4095, sigma=3.0, seed=0x3C5, device=dev))
