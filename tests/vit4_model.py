@@ -1,0 +1,215 @@
+"""Executable model of the 4-lane Viterbi row layout (test infrastructure, like vit8_model).
+
+One packet = 4 lanes x 8 dwords x 2 16-bit halves = 64 trellis positions, so a wave holds
+16 rows (k_viterbi3 with kLanes = 4).  Position bits 0..3 live inside the lane (half, dword
+bits 0..2), bits 4 and 5 are lane bits mapped to lane xor 1, 2: DPP quad_perm inside each
+4-lane group.  The column is vit3_model's shift-free step5
+(labels rotate: position p holds state rotl6(p, t mod 6); partner bit 5 - t mod 6), so the
+half format, markers, snapshot bytes and traceback are unchanged; what changes is which
+partner is a DPP move (phases 0..2), a dword swap (phases 3, 4: dword d ^ 2, d ^ 1) or the
+half swap (phase 5), and which dwords share a branch-metric word:
+  a position bit flips state bit (b + ph) % 6, and flipping state bit 3 changes neither
+  expected bit nor the marker, bit 5 only the marker, two bits that each flip A and B
+  (bits 1, 2) nothing — see bx_source().
+Reference semantics: csrc/sora_ext_viterbi.cpp:66-153 over csrc/viterbicore.hpp:105-239.
+"""
+import numpy as np
+
+from tests import vit3_model as V3
+
+RING = V3.RING
+NL, ND = 4, 8
+XOR_OF_BIT = {4: 1, 5: 2}   # position bit -> lane xor (quad_perm / quad_perm)
+DW_BITS = 3
+
+
+def lane_of(p):
+    l = 0
+    for b, x in XOR_OF_BIT.items():
+        if (p >> b) & 1:
+            l ^= x
+    return l
+
+
+def pos_of(lane, d, h):
+    return h | (d << 1) | ((lane & 1) << 4) | (((lane >> 1) & 1) << 5)
+
+
+POS = np.array([[[pos_of(l, d, h) for h in range(2)] for d in range(ND)] for l in range(NL)])
+assert sorted(POS.ravel().tolist()) == list(range(64))
+assert all(lane_of(pos_of(l, d, h)) == l for l in range(NL) for d in range(ND) for h in range(2))
+
+
+def expected(j):
+    """(A, B, marker) of state j (encoding.blk:92-109; marker = branch index j >> 5)."""
+    return ((j >> 1) ^ (j >> 2) ^ (j >> 4)) & 1, (j ^ (j >> 1) ^ (j >> 2)) & 1, (j >> 5) & 1
+
+
+def sel_word(ph, l, d, k7=False):
+    """v_perm selector of (phase, lane, dword): [BM_hi][bm_hi<<7][BM_lo][bm_lo<<7]
+    (k7: the snapshot-column form [BM + bm][0], byte 4 + 2A + B of {P | 0x01010101 : P})."""
+    w = 0
+    for h in range(2):
+        j = V3.rotl6(int(POS[l, d, h]), ph)
+        A, B, bm = expected(j)
+        if k7:
+            w |= 12 << (16 * h)
+            w |= (2 * A + B + (4 if bm else 0)) << (16 * h + 8)
+        else:
+            w |= (4 if bm else 12) << (16 * h)
+            w |= (2 * A + B) << (16 * h + 8)
+    return w
+
+
+SEL = np.array([[[sel_word(ph, l, d) for d in range(ND)] for l in range(NL)] for ph in range(6)], np.uint32)
+
+
+def bx_source(ph, d):
+    """How column phase ph gets dword d's branch-metric word: ('perm',) its own v_perm,
+    ('same', e) dword e's word, ('mk', e) dword e's word with the marker bits flipped.
+    Derived from which state bits dword bits 0/1 flip at this phase."""
+    flips = [(b + 1 + ph) % 6 for b in range(DW_BITS) if (d >> b) & 1]
+    a_flip = sum(1 for b in flips if b in (1, 2, 4)) & 1
+    b_flip = sum(1 for b in flips if b in (0, 1, 2)) & 1
+    m_flip = sum(1 for b in flips if b == 5) & 1
+    if d == 0:
+        return ("perm",)
+    if a_flip == 0 and b_flip == 0:
+        return ("mk", 0) if m_flip else ("same", 0)
+    # another dword with the same (A, B) flips, if any, lower first
+    for e in range(1, d):
+        fe = [(b + 1 + ph) % 6 for b in range(DW_BITS) if (e >> b) & 1]
+        ae = sum(1 for b in fe if b in (1, 2, 4)) & 1
+        be = sum(1 for b in fe if b in (0, 1, 2)) & 1
+        me = sum(1 for b in fe if b == 5) & 1
+        if (ae, be) == (a_flip, b_flip):
+            return ("mk", e) if me != m_flip else ("same", e)
+    return ("perm",)
+
+
+def partner(T, ph):
+    """T [NL, ND] -> the partner's word for every (lane, dword) at phase ph (the half swap of
+    phase 5 is applied by the caller's op_sel add)."""
+    bit = 5 - ph
+    if bit > DW_BITS:
+        return T[np.arange(NL) ^ XOR_OF_BIT[bit]]
+    if bit >= 1:
+        return T[:, np.arange(ND) ^ (1 << (bit - 1))]
+    return None
+
+
+class Packet(V3.Packet):
+    def __init__(self, frame_len, code_rate):
+        self.fl, self.cr = frame_len, code_rate
+        st = np.where(POS == 0, 0, 48).astype(np.uint32)
+        self.M = ((st[..., 1] << 24) | (st[..., 0] << 8)).astype(np.uint32)   # [4, 8]
+        self.ring = np.zeros((RING, 64), np.uint8)
+        self.tr = 0
+        self.ob = 0
+        self.end = 8 * frame_len + 6
+        self.out = []
+        self.done = False
+        self.v5 = True
+
+    def step5(self, kind, a, b):
+        ph = self.tr % 6
+        c = self.tr + 1
+        k = (c + 1) % 8
+        T = (self.M & (0xFE00FE00 if k == 0 else 0xFFFEFFFF)).astype(np.uint32)
+        mk = 2 << k
+        P = V3.p_word(kind, a, b)
+        BX = np.zeros((NL, ND), np.uint32)
+        mbits = 0x01000100 if k == 7 else mk * 0x00010001
+        for d in range(ND):
+            src = bx_source(ph, d)
+            if src[0] == "perm":
+                if k == 7:
+                    BX[:, d] = V3.perm(P | 0x01010101, P, [sel_word(ph, l, d, k7=True) for l in range(NL)])
+                else:
+                    BX[:, d] = V3.perm(mk * 0x01010101, P, SEL[ph, :, d])
+            elif src[0] == "same":
+                BX[:, d] = BX[:, src[1]]
+            else:
+                BX[:, d] = BX[:, src[1]] ^ mbits
+        K = 28 if kind == V3.FULL else 14
+        C = ((K + 1) << 8) * 0x00010001 if k == 7 else ((K << 8) | mk) * 0x00010001
+        BY = ((C - BX.astype(np.int64)) & 0xFFFFFFFF).astype(np.uint32)
+        add = lambda x, y: ((x.astype(np.uint64) + y) & 0xFFFFFFFF).astype(np.uint32)
+        Tp = partner(T, ph)
+        Z = V3.pk_add(V3.swap_halves(T), BY) if Tp is None else add(Tp, BY)
+        X = add(T, BX)
+        self.M = V3.pk_min(X, Z)
+        self.tr += 1
+        if self.tr % 8 == 6:
+            slot = ((self.tr - 6) // 8) % RING
+            for l in range(NL):
+                for d in range(ND):
+                    for h in range(2):
+                        s = V3.rotl6(int(POS[l, d, h]), self.tr)
+                        self.ring[slot, s] = (int(self.M[l, d]) >> (16 * h + 1)) & 0xFF
+
+    def traceback(self, Mt, T, cnt, look):
+        # the v3 traceback over this layout's positions
+        best = None
+        for l in range(NL):
+            for d in range(ND):
+                for h in range(2):
+                    half = (int(Mt[l, d]) >> (16 * h)) & 0xFFFF
+                    s = V3.rotl6(int(POS[l, d, h]), T)
+                    m = ((half >> 8) & 0xFE) | ((half >> ((T + 1) % 8 + 1)) & 1)
+                    n = (T - 6) % 8
+                    pad = (((half >> 1) & ((1 << n) - 1)) << (8 - n)) & 0xFF
+                    key = ((m << 8) | (4 * s)) & 0xFFFF
+                    key = key - 65536 if key >= 32768 else key
+                    if best is None or key < best[0]:
+                        best = (key, s, pad)
+        _, s, pad = best
+        Z = s | (V3.bitrev(pad, 8) << 6)
+        c_hi = T - look
+        c_first = c_hi - cnt + 8
+        C0 = T - ((T - 6) % 8)
+        sc = (Z >> (T - C0)) & 63
+        blocks = {}
+        C = C0
+        while C >= c_first:
+            b = int(self.ring[((C - 6) // 8) % RING, sc])
+            if C <= c_hi:
+                blocks[C] = b
+            sc = V3.bitrev(b & 63, 6)
+            C -= 8
+        return [blocks[c] for c in range(c_first, c_hi + 1, 8)]
+
+
+def decode(soft, frame_len, code_rate):
+    """Model of one packet through the 8-lane layout (vit3_model.decode's driver loop)."""
+    P = Packet(frame_len, code_rate)
+    kinds = V3.KINDS[code_rate]
+    G = {0: 2, 1: 3, 2: 4}[code_rate]
+    soft = np.asarray(soft, np.int64)
+    pend = None
+    for g in range(soft.size // G):
+        s = soft[g * G:(g + 1) * G]
+        args = [(s[0], s[1])] + [(v, 0) for v in s[2:]]
+        for k, kind in enumerate(kinds):
+            P.step5(kind, *args[k])
+        if P.tr % 8 == 0:
+            P.normalize()
+        if P.tr >= P.end:
+            if pend is not None:
+                P.out += P.traceback(*pend)
+                pend = None
+            cnt = P.end - P.ob - 6
+            if cnt:
+                P.out += P.traceback(P.M, P.tr, cnt, P.tr - P.end)
+            P.done = True
+            break
+        if P.tr >= P.ob + 286:
+            assert pend is None
+            pend = (P.M.copy(), P.tr, 256, 24 + (P.tr - P.ob - 286) % 8)
+            P.ob += 256
+        if pend is not None and P.tr % 24 == 0:
+            P.out += P.traceback(*pend)
+            pend = None
+    if pend is not None:
+        P.out += P.traceback(*pend)
+    return np.array(P.out, np.uint8)

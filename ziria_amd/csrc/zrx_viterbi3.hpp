@@ -44,16 +44,16 @@ namespace v3 {
 #define ZRX_VLANES 8
 #endif
 constexpr int kLanes = ZRX_VLANES;                     // lanes per row (packet): 8 or 16
-static_assert(kLanes == 8 || kLanes == 16, "rows are 8 or 16 lanes");
+static_assert(kLanes == 4 || kLanes == 8 || kLanes == 16, "rows are 4, 8 or 16 lanes");
 constexpr int kDw = 32 / kLanes;                       // dwords per lane: 4 or 2
-constexpr int kDwBits = kLanes == 8 ? 2 : 1;           // position bits 1..kDwBits = the dword
-constexpr int kLaneBits = kLanes == 8 ? 3 : 4;
+constexpr int kDwBits = kLanes == 4 ? 3 : kLanes == 8 ? 2 : 1;   // position bits 1..kDwBits = the dword
+constexpr int kLaneBits = kLanes == 4 ? 2 : kLanes == 8 ? 3 : 4;
 constexpr int kRowsWave = 64 / kLanes;                 // rows per wave
 constexpr uint32_t kRowMask = (1u << kLanes) - 1u;     // a row's lanes in a ballot (shifted)
 constexpr int kRing = 39;                 // snapshot slots of 8 columns per packet (>= 38)
 constexpr int kRows = 4 * kRowsWave;      // packets per 256-thread block
 constexpr int kSlotBytes = kRows * 64;
-constexpr int kWavesPerSimd = kLanes == 8 ? 2 : 4;     // LDS ring: 16 rows per SIMD
+constexpr int kWavesPerSimd = kLanes == 4 ? 1 : kLanes == 8 ? 2 : 4;   // LDS ring: 16 rows per SIMD
 constexpr uint32_t kNever = 0x7FFFFFFFu;
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -71,6 +71,7 @@ __host__ __device__ constexpr uint32_t rev6(uint32_t x) {
 // position held by (lane-in-row l, dword d, half h)
 //   8 lanes:  lane = b3*1 ^ b4*2 ^ b5*7        16 lanes: lane = b2*1 ^ b3*2 ^ b4*15 ^ b5*8
 __host__ __device__ constexpr uint32_t pos_of(uint32_t l, uint32_t d, uint32_t h) {
+  if (kLanes == 4) return h | (d << 1) | ((l & 1u) << 4) | (((l >> 1) & 1u) << 5);   // lane = b4*1 ^ b5*2
   if (kLanes == 8) {
     const uint32_t b5 = (l >> 2) & 1u;
     const uint32_t b3 = (l & 1u) ^ b5, b4 = ((l >> 1) & 1u) ^ b5;
@@ -82,7 +83,8 @@ __host__ __device__ constexpr uint32_t pos_of(uint32_t l, uint32_t d, uint32_t h
 }
 // DPP control of the cross-lane partner for position bit pb (> kDwBits)
 __host__ __device__ constexpr int partner_dpp(int pb) {
-  return kLanes == 8 ? (pb == 5 ? 0x141 : pb == 4 ? 0x4E : 0xB1)
+  return kLanes == 4 ? (pb == 5 ? 0x4E : 0xB1)
+       : kLanes == 8 ? (pb == 5 ? 0x141 : pb == 4 ? 0x4E : 0xB1)
                      : (pb == 5 ? 0x128 : pb == 4 ? 0x140 : pb == 3 ? 0x4E : 0xB1);
 }
 // Branch-metric word sharing (tests/vit8_model.py bx_source): the state bits dword d's
@@ -232,7 +234,7 @@ __device__ __forceinline__ void normalize(uint32_t (&M)[kDw]) {
   uint32_t v = (uint32_t)min(t.x, t.y);
   v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
   v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
-  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));
+  if constexpr (kLanes >= 8) v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));
   if constexpr (kLanes == 16) v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false));
   const uint32_t rep = __builtin_amdgcn_perm(0u, v, 0x010C010Cu);   // [H][0][H][0]
 #pragma unroll
@@ -541,7 +543,7 @@ __device__ __forceinline__ void traceback(bool due, const uint32_t (&M)[kDw], ui
   }
   best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0xB1, 0xF, 0xF, false));
   best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x4E, 0xF, 0xF, false));
-  best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x141, 0xF, 0xF, false));
+  if constexpr (kLanes >= 8) best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x141, 0xF, 0xF, false));
   if constexpr (kLanes == 16) best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x140, 0xF, 0xF, false));
   const bool walker = due && l == 0 && cnt != 0;
   const uint64_t wm = __builtin_amdgcn_ballot_w64(walker);
@@ -668,7 +670,8 @@ constexpr int kPw = (24 + kLanes - 1) / kLanes;        // P words a lane builds 
 #ifndef ZRX_DWFETCH
 #define ZRX_DWFETCH 1
 #endif
-constexpr bool kDwFetch = kLanes == 8 && ZRX_DWFETCH != 0;
+constexpr bool kDwFetch = kLanes <= 8 && ZRX_DWFETCH != 0;
+constexpr int kCpl = 24 / kLanes;                      // (kDwFetch) body columns a lane builds P words for
 #ifndef ZRX_VPF
 #define ZRX_VPF 1
 #endif
@@ -691,8 +694,8 @@ struct Packet {
   // P word of body column J: lane J mod kLanes of the row built it as its word J / kLanes
   template <int J>
   static __device__ __forceinline__ uint32_t bcast(const uint32_t (&Pw)[kPw]) {
-    if constexpr (kDwFetch)   // lane J / 3 built columns 3l .. 3l + 2
-      return (uint32_t)__builtin_amdgcn_ds_swizzle((int)Pw[J % 3], ((J / 3) << 5) | (32 - kLanes));
+    if constexpr (kDwFetch)   // lane J / kCpl built columns kCpl l .. kCpl l + kCpl - 1
+      return (uint32_t)__builtin_amdgcn_ds_swizzle((int)Pw[J % kCpl], ((J / kCpl) << 5) | (32 - kLanes));
     else
       return (uint32_t)__builtin_amdgcn_ds_swizzle((int)Pw[J / kLanes], ((J % kLanes) << 5) | (32 - kLanes));
   }
@@ -779,6 +782,11 @@ static __device__ __forceinline__ void ds_b8_hi(uint32_t a, uint32_t v) {
   }
 };
 
+// soft offset (within a body chunk) of body column j (constexpr form)
+__host__ __device__ constexpr uint32_t soft_off_c(int cr, int j) {
+  const int st = cr == 0 ? 1 : cr == 1 ? 2 : 3, G = cr == 0 ? 2 : cr == 1 ? 3 : 4;
+  return (uint32_t)((j / st) * G + (j % st == 0 ? 0 : j % st + 1));
+}
 // soft offset (within a body chunk) and kind of body column j
 template <int CR>
 __device__ __forceinline__ uint32_t soft_off(uint32_t j) {
@@ -832,17 +840,24 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
   PKind kd[kPw];
   // kDwFetch: dwords dw0, +4, +8 hold this lane's bytes; word i's a / b are bytes sa_/sb_ of
   // {D1:D0} (or {D2:D1} for word 2 at rate 1/2)
-  constexpr int nD = kDwFetch ? (CR == 0 ? 3 : 2) : 2 * kPw;
+  // 8 lanes: 2 dwords (3 at rate 1/2, word 2 from {D2:D1}); 4 lanes: word i from the pair
+  // {D(k+1):Dk}, k = its first byte / 4 (the columns' byte offsets from column kCpl l repeat
+  // every 6 columns, so k is a constant)
+  constexpr int nD = !kDwFetch ? 2 * kPw : kLanes == 8 ? (CR == 0 ? 3 : 2) : (CR == 2 ? 3 : 4);
   uint32_t vo[kDwFetch ? 1 : kPw], selA[kPw], selB[kPw];
   if constexpr (kDwFetch) {
-    const uint32_t j0 = 3u * l, off0 = soft_off<CR>(j0);
+    const uint32_t j0 = (uint32_t)kCpl * l, off0 = soft_off<CR>(j0);
     const uint32_t w0 = rel + off0, sh = w0 & 3u;
     vo[0] = w0 & ~3u;
 #pragma unroll
     for (int i = 0; i < kPw; i++) {
       kd[i] = p_kind((j0 + i) % RT::steps);
       uint32_t q = soft_off<CR>(j0 + i) - off0 + sh;
-      if (CR == 0 && i == 2) q -= 4u;                  // from {D2:D1}
+      if constexpr (kLanes == 8) {
+        if (CR == 0 && i == 2) q -= 4u;                // from {D2:D1}
+      } else {
+        q -= 4u * (soft_off<CR>((uint32_t)i) >> 2);    // from the pair holding byte soft_off(i)
+      }
       selA[i] = q * 0x01010101u;
       selB[i] = (q + 1u) * 0x01010101u;
     }
@@ -876,8 +891,8 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
 #pragma unroll
     for (int i = 0; i < kPw; i++) {
       if constexpr (kDwFetch) {
-        const uint32_t lo = (CR == 0 && i == 2) ? sd[0][1] : sd[0][0], hi = (CR == 0 && i == 2) ? sd[0][2] : sd[0][1];
-        Pw[i] = p_word_sel(kd[i], hi, lo, selA[i], selB[i]);
+        const int k = kLanes == 8 ? ((CR == 0 && i == 2) ? 1 : 0) : (int)(soft_off_c(CR, i) >> 2);
+        Pw[i] = p_word_sel(kd[i], sd[0][k + 1], sd[0][k], selA[i], selB[i]);
       } else {
         Pw[i] = p_word(kd[i], sd[0][2 * i], sd[0][2 * i + 1]);
       }
