@@ -730,9 +730,9 @@ static __device__ __forceinline__ void ds_b8_hi(uint32_t a, uint32_t v) {
     } else {
       // byte stores at constant offsets from one address: half 0 by a plain store (the
       // compiler emits and schedules ds_write_b8), half 1 by ds_write_b8_d16_hi (the
-      // compiler would shift first).  The asm has no memory clobber (one cost 0.7-1.5 %):
-      // nothing in the body reads a slot its snapshots write, and the tracebacks that do
-      // run after the body's branch.
+      // compiler would shift first).  The asm has no memory clobber (one per store cost
+      // 0.7-1.5 %); the ordering that matters is kept by compiler barriers at the body's end
+      // and, in bodies with a deferred walk, after each snapshot (col, body).
       uint8_t* b = s + K.sa[k];
       ((b[snap_delta(k, D, 0)] = (uint8_t)u[D]), ...);
       const uint32_t a = lds_addr(s) + K.sa[k];
@@ -754,7 +754,13 @@ static __device__ __forceinline__ void ds_b8_hi(uint32_t a, uint32_t v) {
     constexpr int r = J % RT::steps;
     constexpr int c = J + 1;                           // column index within the body after the step
     column5<J % 6, r, (J + 2) % 8>(M, P, K);
-    if constexpr (c % 8 == 6 && !(DBG & 2)) snapshot<(c >> 3)>(M, std::make_integer_sequence<int, kDw>{});
+    if constexpr (c % 8 == 6 && !(DBG & 2)) {
+      snapshot<(c >> 3)>(M, std::make_integer_sequence<int, kDw>{});
+      // A deferred walk (WE > 0) reads, in this body, slots that this body's snapshots then
+      // overwrite: its loads must stay ahead of the half-1 asm stores, which the compiler
+      // cannot see as memory writes
+      if constexpr (WE > 0) asm volatile("" ::: "memory");
+    }
     if constexpr (c % RT::steps == 0) {                // group end
       if constexpr (c % 8 == 0 && (CR != 2 || c == 24) && !(DBG & 4)) normalize(M);
       if constexpr (CHECKED) {
@@ -779,6 +785,9 @@ static __device__ __forceinline__ void ds_b8_hi(uint32_t a, uint32_t v) {
     uint32_t Pq[kPq];
     if constexpr (!(DBG & 8)) pq_fill(Pq, Pw, std::make_integer_sequence<int, kPq>{});
     (col<J, CHECKED, WE>(M, Pq, Pw, tr0, s_next), ...);
+    // the tracebacks after a body read the slots its snapshots wrote (half 1 by asm stores
+    // without a memory clobber): no load moves above this point
+    asm volatile("" ::: "memory");
   }
 };
 
