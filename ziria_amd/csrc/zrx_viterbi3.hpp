@@ -818,10 +818,17 @@ __device__ __forceinline__ int64_t wave_max_rows64(int64_t v) {
   return m;
 }
 
+#ifndef ZRX_PRIO_NUM
+#define ZRX_PRIO_NUM 2
+#endif
+#ifndef ZRX_PRIO_DEN
+#define ZRX_PRIO_DEN 3
+#endif
+constexpr int kPrioNum = ZRX_PRIO_NUM, kPrioDen = ZRX_PRIO_DEN;
 template <int CR, int DBG>
 __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64_t so, uint32_t n, Row& R, const Consts& K, uint32_t l,
                          uint32_t rib, uint8_t* ring_block, uint8_t* __restrict__ out, uint32_t ooff,
-                         uint32_t (&M)[kDw], RowX* rowx, uint2* __restrict__ dumps) {
+                         uint32_t (&M)[kDw], RowX* rowx, uint2* __restrict__ dumps, bool younger) {
   using RT = Rate<CR>;
   Walk W;
   W.we = 0;
@@ -920,10 +927,22 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
   uint32_t slot = 0;                                   // first slot of this body (3 per body)
   uint32_t tr0 = 0, base = 0;
   constexpr auto cols24 = std::make_integer_sequence<int, 24>{};
+  // Issue priority (ZRX_PRIO_NUM / ZRX_PRIO_DEN): a SIMD's two waves come from blocks b and
+  // b + ncu, and with equal priority the SIMD always issues the older one first, so it runs
+  // at nearly full speed and the younger one finishes alone long after it.  The younger
+  // wave (odd block round) raises its priority in NUM of every DEN bodies.
+  uint32_t pc = 0;
   auto next_body = [&]() {
     slot = slot + 3 == kRing ? 0 : slot + 3;
     tr0 += 24;
     base += RT::chunk;
+    if constexpr (kPrioNum > 0) {
+      if (younger) {
+        pc = pc + 1 == (uint32_t)kPrioDen ? 0u : pc + 1;
+        if (pc < (uint32_t)kPrioNum) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      }
+    }
   };
   while (__builtin_amdgcn_ballot_w64(R.live) != 0) {
     // The hot loop: bodies with no event due, no deferred walk, nothing else on this path
@@ -1131,9 +1150,9 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
         for (int d = 0; d < v3::kDw; d++) Rr.pM[d] = Rr.fM[d] = 0u;
         Rr.nbytes = 0;
         Rr.next = v3::row_next(Rr);
-        if (rate == 0) v3::run_rows<0, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M, rowx, dumps);
-        else if (rate == 1) v3::run_rows<1, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M, rowx, dumps);
-        else v3::run_rows<2, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M, rowx, dumps);
+        if (rate == 0) v3::run_rows<0, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M, rowx, dumps, !FIX && ((blockIdx.x / ncu) & 1u) != 0u);
+        else if (rate == 1) v3::run_rows<1, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M, rowx, dumps, !FIX && ((blockIdx.x / ncu) & 1u) != 0u);
+        else v3::run_rows<2, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M, rowx, dumps, !FIX && ((blockIdx.x / ncu) & 1u) != 0u);
         if (mq) nbytes = Rr.nbytes;
       }
     }
