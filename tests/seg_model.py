@@ -57,6 +57,31 @@ def seg_stop(E, cols, nseg, k):
     return seg_start(E, nseg, k + 1) + WARM + 30 if k + 1 < nseg else cols
 
 
+def order_place(pos, nfull, ncu, rows=32):
+    """v3::order_place: sorted position -> row slot, whole blocks snake over ncu CUs."""
+    b = pos // rows
+    if b >= nfull:
+        return pos
+    r, c = divmod(b, ncu)
+    base = r * ncu
+    m = min(ncu, nfull - base)
+    return ((base + m - 1 - c) if r & 1 else b) * rows + pos % rows
+
+
+def rank_place(r, nfull, ncu, rows=32):
+    """v3::rank_place: block rank (0 = longest) -> block slot (blocks dealt to CU slot mod ncu)."""
+    if nfull <= ncu:
+        return r
+    if nfull <= 2 * ncu:
+        n2 = nfull - ncu
+        alone = ncu - n2
+        if r < alone:
+            return ncu - 1 - r
+        q = r - alone
+        return q if q < n2 else ncu + (2 * n2 - 1 - q)
+    return order_place(r * rows, nfull, ncu, rows) // rows
+
+
 def std_init():
     m = np.full(64, 48, np.int64)
     m[0] = 0

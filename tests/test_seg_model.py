@@ -49,6 +49,30 @@ def test_row_bound():
         assert rows <= min(n + r + r // 256 + 64, n * SM.MAX_SEG), (it, n, rows)
 
 
+def test_rank_place():
+    """The ranked block placement of a mixed batch (v3::rank_place, restated in seg_model) is a
+    permutation of the whole blocks; up to two rounds, the longest blocks sit alone on the CUs
+    the second round leaves free (the partial last block's CU getting the shortest of them),
+    and every other CU holds ranks summing to the same total (longest with shortest)."""
+    for ncu in (2, 3, 8, 256):
+        for nfull in list(range(1, 3 * ncu + 3)) if ncu < 256 else (1, 255, 256, 257, 300, 496, 511, 512, 513, 900):
+            slots = [SM.rank_place(r, nfull, ncu) for r in range(nfull)]
+            assert sorted(slots) == list(range(nfull)), (ncu, nfull)
+            if ncu < nfull <= 2 * ncu:
+                n2 = nfull - ncu
+                cu = {}
+                for r, s in enumerate(slots):
+                    cu.setdefault(s % ncu, []).append(r)
+                alone = [v for v in cu.values() if len(v) == 1]
+                pairs = [v for v in cu.values() if len(v) == 2]
+                assert len(pairs) == n2 and len(alone) == ncu - n2
+                if alone:                                      # the longest alone
+                    assert max(v[0] for v in alone) < min(min(v) for v in pairs)
+                assert len({sum(v) for v in pairs}) == 1
+                if ncu - n2 > 0:                               # CU n2 (the partial block's) gets the shortest alone
+                    assert cu[n2] == [ncu - n2 - 1]
+
+
 CASES = [(cr, fl, noise, nseg) for cr in (0, 1, 2) for fl, noise, nseg in
          [(400, 0, 2), (700, 3, 3), (1100, 2, 5), (700, -1, 3), (1100, -1, 5)]]
 

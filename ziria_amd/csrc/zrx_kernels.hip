@@ -232,6 +232,9 @@ __global__ __launch_bounds__(256) void k_signal_vit(const uint32_t* __restrict__
 // segment length from the batch's column total, the packet keys counted in one pass and
 // scattered in another, and the rows expanded from the sorted packets by a block scan.
 constexpr int kScanPer = 16;
+#ifndef ZRX_RANK_BLOCKS
+#define ZRX_RANK_BLOCKS 1   // (0: A/B builds without the ranked block placement)
+#endif
 #ifndef ZRX_PLAN_CUT
 #define ZRX_PLAN_CUT 99   // (scripts/ubench/plan_ubench.hip: time k_pkt_plan up to one of its phases)
 #endif
@@ -287,8 +290,8 @@ __device__ __forceinline__ void plan_pkts(const int32_t* __restrict__ vparams, i
 // The mixed batch's rows (k_pkt_plan's comment): packets keyed by (rate, segment length)
 // with segment length Lm, counted and scattered in LDS (hist: kOrderPerThread x 1024 words,
 // zeroed; *rtotal zeroed), then expanded onto rows by a block scan.  1024 threads.
-// (Tried: row blocks re-ranked by length across the rates before the snake placement;
-// config 5's Viterbi 0.672 -> 0.75 ms.)
+// (Ranked placement, interleaved A/B on config 5: Viterbi 0.637-0.648 -> 0.597-0.629 ms; an
+// earlier version that re-ranked waves and blocks inside the snake measured 0.672 -> 0.75.)
 __device__ __forceinline__ void plan_rows_mixed(const int32_t* __restrict__ vparams, int npkts, uint32_t Lm,
                                                 int2* __restrict__ rows, int32_t* __restrict__ nrows,
                                                 uint8_t* __restrict__ segs, int32_t* __restrict__ order,
@@ -304,37 +307,82 @@ __device__ __forceinline__ void plan_rows_mixed(const int32_t* __restrict__ vpar
   __syncthreads();                                     // order[] and segs[] written by the block
   if (ZRX_PLAN_CUT <= 5) return;
   // Expand: the segments of the packet at sorted position i are rows prefix(i) .. +nseg - 1
-  // (consecutive, so a wave holds segments of one or two packets of similar length), placed
-  // snake over the CUs.  Thread t takes positions 16t .. 16t + 15 of each round.
+  // (consecutive, so a wave holds segments of one or two packets of similar length).  Thread
+  // t takes positions 16t .. 16t + 15 of each round.  Two sweeps: the first finds each whole
+  // block's longest row (blk[]), the blocks are ranked by it and placed (v3::rank_place), and
+  // the second writes the rows there.  (Sorted by rate first, the blocks' lengths rise and
+  // fall three times, and the snake over that order paired long blocks with long ones: config
+  // 5's per-SIMD columns spread 768..11 614 around a mean of 9026.)
   const uint32_t total = *rtotal, nfull = total / (uint32_t)v3::kRows;
   const uint32_t ncu2 = (uint32_t)max(ncu, 2), ncu_rcp = 0xFFFFFFFFu / ncu2 + 1u;
+  const bool ranked = ZRX_RANK_BLOCKS && nfull <= (uint32_t)v3::kRankBlocks;
   __shared__ uint32_t esum[16];
-  uint32_t carry = 0;
-  for (uint32_t base = 0; base < npk; base += 1024u * kScanPer) {
-    int32_t pk[kScanPer];
-    uint32_t ns[kScanPer], sum = 0;
+  __shared__ uint32_t blk[v3::kRankBlocks];           // longest row, then the placed slot
+  if (ranked)
+    for (uint32_t b = t; b < nfull; b += 1024u) blk[b] = 0u;
+  __syncthreads();
+  for (int sweep = ranked ? 0 : 1; sweep < 2; sweep++) {
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < npk; base += 1024u * kScanPer) {
+      int32_t pk[kScanPer];
+      uint32_t ns[kScanPer], sum = 0;
 #pragma unroll
-    for (int i = 0; i < kScanPer; i++) {
-      const uint32_t pos = base + kScanPer * (uint32_t)t + i;
-      pk[i] = pos < npk ? order[pos] : -1;
-    }
-#pragma unroll
-    for (int i = 0; i < kScanPer; i++) { ns[i] = pk[i] >= 0 ? segs[pk[i]] : 0u; sum += ns[i]; }
-    const uint32_t inc = wave_incl_scan(sum);
-    if (lane == 63) esum[wv] = inc;
-    __syncthreads();
-    uint32_t ex = carry + inc - sum, rnd = 0;
-    for (int w = 0; w < 16; w++) { ex += w < wv ? esum[w] : 0u; rnd += esum[w]; }
-#pragma unroll
-    for (int i = 0; i < kScanPer; i++) {
-      for (uint32_t k = 0; k < ns[i]; k++) {
-        const uint32_t at = v3::order_place(ex + k, nfull, ncu2, ncu_rcp);
-        if (at < (uint32_t)rows_cap) rows[at] = make_int2(pk[i], (int)(k | (ns[i] << 8)));   // (always: the plan's row bound)
+      for (int i = 0; i < kScanPer; i++) {
+        const uint32_t pos = base + kScanPer * (uint32_t)t + i;
+        pk[i] = pos < npk ? order[pos] : -1;
       }
-      ex += ns[i];
+#pragma unroll
+      for (int i = 0; i < kScanPer; i++) { ns[i] = pk[i] >= 0 ? segs[pk[i]] : 0u; sum += ns[i]; }
+      const uint32_t inc = wave_incl_scan(sum);
+      if (lane == 63) esum[wv] = inc;
+      __syncthreads();
+      uint32_t ex = carry + inc - sum, rnd = 0;
+      for (int w = 0; w < 16; w++) { ex += w < wv ? esum[w] : 0u; rnd += esum[w]; }
+#pragma unroll
+      for (int i = 0; i < kScanPer; i++) {
+        if (sweep == 0) {
+          if (ns[i] != 0u) {                           // the row length the sort keyed on
+            const int4 q = *reinterpret_cast<const int4*>(vparams + 4 * (int64_t)pk[i]);
+            const uint32_t cols = cols_of(q.y, q.z);
+            const uint32_t len = ns[i] <= 1u ? cols : v3::udiv_small(min(cols, (1u << 20) - 1u) + ns[i] - 1u, ns[i]) + 286u;
+            for (uint32_t b = ex / (uint32_t)v3::kRows; b * (uint32_t)v3::kRows < ex + ns[i] && b < nfull; b++)
+              atomicMax(&blk[b], len);
+          }
+        } else {
+          for (uint32_t k = 0; k < ns[i]; k++) {
+            const uint32_t pos = ex + k, b = pos / (uint32_t)v3::kRows;
+            const uint32_t at = !ranked ? v3::order_place(pos, nfull, ncu2, ncu_rcp)
+                                : b < nfull ? blk[b] * (uint32_t)v3::kRows + pos % (uint32_t)v3::kRows : pos;
+            if (at < (uint32_t)rows_cap) rows[at] = make_int2(pk[i], (int)(k | (ns[i] << 8)));   // (always: the plan's row bound)
+          }
+        }
+        ex += ns[i];
+      }
+      carry += rnd;
+      __syncthreads();                                 // esum is rewritten by the next round
     }
-    carry += rnd;
-    __syncthreads();                                   // esum is rewritten by the next round
+    if (sweep == 0) {
+      // rank the whole blocks by their longest row, longest first (a counting sort over
+      // 24-column bodies in hist[0 .. 1023]; ties in any order), then place them
+      for (int i = t; i < kOrderPerThread * 1024; i += 1024) hist[i] = 0;
+      __syncthreads();
+      for (uint32_t b0 = 0; b0 < nfull; b0 += 1024u) {
+        const uint32_t b = b0 + (uint32_t)t;
+        const uint32_t key = b < nfull ? (uint32_t)kOrderLen - 1u - min((blk[b] + 23u) / 24u, (uint32_t)kOrderLen - 1u) : 0u;
+        if (b < nfull) atomicAdd(&hist[key], 1u);
+      }
+      __syncthreads();
+      order_hist_scan(hist);
+      __syncthreads();
+      for (uint32_t b0 = 0; b0 < nfull; b0 += 1024u) {
+        const uint32_t b = b0 + (uint32_t)t;
+        const uint32_t key = b < nfull ? (uint32_t)kOrderLen - 1u - min((blk[b] + 23u) / 24u, (uint32_t)kOrderLen - 1u) : 0u;
+        const uint32_t r = order_claim(hist, b < nfull, key);
+        __syncthreads();                               // every lane read blk[] before it is rewritten
+        if (b < nfull) blk[b] = v3::rank_place(r, nfull, ncu2, ncu_rcp);
+      }
+      __syncthreads();
+    }
   }
   if (t == 0) {
     nrows[v3::kPlanRows] = (int32_t)min(total, (uint32_t)rows_cap);

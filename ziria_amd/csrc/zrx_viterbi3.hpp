@@ -329,6 +329,22 @@ __host__ __device__ __forceinline__ uint32_t order_place(uint32_t pos, uint32_t 
   const uint32_t m = min(ncu, nfull - base);
   return ((r & 1u) ? base + m - 1u - c : b) * (uint32_t)kRows + pos % (uint32_t)kRows;
 }
+// A mixed batch's whole blocks ranked by their longest row (0 = longest; plan_rows_mixed)
+// -> block slot, for blocks dealt to CU slot mod ncu.  Up to two rounds: the longest blocks
+// alone on the CUs the second round leaves free (the shortest of them on the CU that also
+// gets the partial last block, slot nfull), the rest paired longest with shortest.  More
+// rounds: the snake of order_place over the ranks.  A permutation of 0 .. nfull - 1.
+constexpr int kRankBlocks = 4096;                      // ranked when the batch has at most this many
+__host__ __device__ __forceinline__ uint32_t rank_place(uint32_t r, uint32_t nfull, uint32_t ncu, uint32_t rcp) {
+  if (nfull <= ncu) return r;
+  if (nfull <= 2u * ncu) {
+    const uint32_t n2 = nfull - ncu, alone = ncu - n2;   // CUs with two whole blocks, with one
+    if (r < alone) return ncu - 1u - r;
+    const uint32_t q = r - alone;                      // CU c: ranks alone + c and alone + 2 n2 - 1 - c
+    return q < n2 ? q : ncu + (2u * n2 - 1u - q);
+  }
+  return order_place(r * (uint32_t)kRows, nfull, ncu, rcp) / (uint32_t)kRows;
+}
 // The plan header k_pkt_plan writes for k_viterbi3 (int32 words of the nrows buffer).
 enum PlanWord { kPlanRows = 0, kPlanFixes = 1, kPlanUniform = 2, kPlanNcu = 3, kPlanSegLen = 4, kPlanDropped = 5 };   // (8 words)
 
@@ -818,17 +834,49 @@ __device__ __forceinline__ int64_t wave_max_rows64(int64_t v) {
   return m;
 }
 
+// Issue priority of a SIMD's waves (run_rows).  ZRX_PRIO_MODE 1: the younger wave (odd block
+// round) raises its priority in ZRX_PRIO_NUM of every ZRX_PRIO_DEN bodies.  2: the wave with
+// the most columns left on its SIMD has it (g_vprog).  3: 2 for a mixed batch's planned rows,
+// 1 otherwise.  0: off.  (Config 5, interleaved A/B with the ranked placement: 3 at 0.584-0.618
+// ms, 1 at 0.597-0.629, within the boxes' spread; 2 on uniform batches: config 3 1.14-1.16 vs
+// 1.13-1.14, config 2 0.41 vs 0.37 — the waves then run in lockstep and meet their
+// traceback events together.  1 stays the default.)
+#ifndef ZRX_PRIO_MODE
+#define ZRX_PRIO_MODE 1
+#endif
 #ifndef ZRX_PRIO_NUM
 #define ZRX_PRIO_NUM 2
 #endif
 #ifndef ZRX_PRIO_DEN
 #define ZRX_PRIO_DEN 3
 #endif
-constexpr int kPrioNum = ZRX_PRIO_NUM, kPrioDen = ZRX_PRIO_DEN;
+constexpr int kPrioMode = ZRX_PRIO_MODE, kPrioNum = ZRX_PRIO_NUM, kPrioDen = ZRX_PRIO_DEN;
+// Columns left per resident wave: 16 words (HW_ID wave slots) per SIMD, the SIMD numbered
+// from HW_ID / XCC_ID as (xcc, se, sh, cu, simd).  A wave writes its own word every body and
+// 0 when it leaves; stale words of earlier launches are 0.  Only a speed hint: a wrong value
+// changes which wave issues first, never what is computed.
+constexpr int kProgSimds = 8 * 1024;
+__device__ uint32_t g_vprog[kProgSimds * 16];
+__device__ __forceinline__ uint32_t* prog_words(uint32_t& wid) {
+  const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+  const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+  wid = hw & 15u;
+  const uint32_t s = (xcc & 7u) * 1024u + ((hw >> 13) & 7u) * 128u + ((hw >> 12) & 1u) * 64u + ((hw >> 8) & 15u) * 4u +
+                     ((hw >> 4) & 3u);
+  return g_vprog + 16u * s;
+}
+// max over the 16 lanes of each DPP row (every lane of the row gets it)
+__device__ __forceinline__ uint32_t row16_max(uint32_t x) {
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xF, 0xF, false));   // row_ror:8
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x124, 0xF, 0xF, false));   // row_ror:4
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x122, 0xF, 0xF, false));   // row_ror:2
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x121, 0xF, 0xF, false));   // row_ror:1
+  return x;
+}
 template <int CR, int DBG>
 __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64_t so, uint32_t n, Row& R, const Consts& K, uint32_t l,
                          uint32_t rib, uint8_t* ring_block, uint8_t* __restrict__ out, uint32_t ooff,
-                         uint32_t (&M)[kDw], RowX* rowx, uint2* __restrict__ dumps, bool younger) {
+                         uint32_t (&M)[kDw], RowX* rowx, uint2* __restrict__ dumps, bool prio, bool younger) {
   using RT = Rate<CR>;
   Walk W;
   W.we = 0;
@@ -927,20 +975,55 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
   uint32_t slot = 0;                                   // first slot of this body (3 per body)
   uint32_t tr0 = 0, base = 0;
   constexpr auto cols24 = std::make_integer_sequence<int, 24>{};
-  // Issue priority (ZRX_PRIO_NUM / ZRX_PRIO_DEN): a SIMD's two waves come from blocks b and
-  // b + ncu, and with equal priority the SIMD always issues the older one first, so it runs
-  // at nearly full speed and the younger one finishes alone long after it.  The younger
-  // wave (odd block round) raises its priority in NUM of every DEN bodies.
+  // Issue priority: a SIMD's two waves come from blocks b and b + ncu, and with equal
+  // priority the SIMD always issues the older one first, so it runs at nearly full speed and
+  // the younger one finishes alone long after it (and in a mixed batch a long wave beside a
+  // short one runs at the shared speed, then alone).  Mode 2: every body, the wave with more
+  // columns left than any other wave on its SIMD (their words loaded one body earlier) takes
+  // priority 1 — longest remaining first, so the SIMD's waves end together and a long wave
+  // beside short ones runs at nearly its lone speed.  Mode 1: the younger wave raises its
+  // priority in NUM of every DEN bodies.
   uint32_t pc = 0;
+  uint32_t wid = 0, pv = 0;
+  uint32_t* const pw = kPrioMode >= 2 && prio ? prog_words(wid) : g_vprog;
+  // the SIMD's 16 words by buffer ops with sc0: read from this XCD's L2, where the other
+  // waves of this CU write them (agent-scope atomics go past the L2 to memory: 1.51 ms
+  // instead of 1.14, whole CUs slowed by the round trips)
+  const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc((void*)pw, (short)0, 64, 0x00020000);
+  constexpr int kSc0 = 1;
+  const uint32_t wend = kPrioMode >= 2 && prio ? (uint32_t)wave_max_rows64(R.live ? (int64_t)R.cols : 0) : 0u;
+  const uint32_t lane = __lane_id();
   auto next_body = [&]() {
     slot = slot + 3 == kRing ? 0 : slot + 3;
     tr0 += 24;
     base += RT::chunk;
-    if constexpr (kPrioNum > 0) {
+    if constexpr (kPrioMode >= 2) {
+      if (prio) {
+        const uint32_t rem = wend > tr0 ? wend - tr0 : 0u;
+        const uint32_t om = (uint32_t)__builtin_amdgcn_readfirstlane((int)row16_max(lane < 16u && lane != wid ? pv : 0u));
+        if (rem > om) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    if constexpr (kPrioMode != 2 && kPrioNum > 0) {
       if (younger) {
         pc = pc + 1 == (uint32_t)kPrioDen ? 0u : pc + 1;
         if (pc < (uint32_t)kPrioNum) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);
+      }
+    }
+  };
+  // Mode 2's own word and the SIMD's words, at the start of a body (before its soft prefetch,
+  // so next_body's wait for pv leaves the prefetch in flight): the store and load then have
+  // the whole body to complete.
+  // (Every lane stores / loads: a lane-masked memory op is a branch, and the waitcnt pass then
+  // drains everything in flight at the loop head; issued at the body's end, the loop head's
+  // wait for the prefetch also waited for them: 1.63 ms instead of 1.14.)
+  auto publish = [&]() {
+    if constexpr (kPrioMode >= 2) {
+      if (prio) {
+        __builtin_amdgcn_raw_buffer_store_b32(wend > tr0 ? wend - tr0 : 0u, prs, (int)(4u * wid), 0, kSc0);
+        pv = __builtin_amdgcn_raw_buffer_load_b32(prs, (int)(4u * (lane & 15u)), 0, kSc0);
       }
     }
   };
@@ -949,6 +1032,7 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
     // (its own loop, so the register allocator keeps the loop-carried values in place).
     while ((DBG & 16) || (s_next > tr0 + 24 && s_next != kNever)) {
       uint32_t Pw[kPw];
+      publish();
       pwords(Pw, base);
       pk.ring = ring_block + slot * kSlotBytes;
       pk.template body<false, 0>(M, Pw, tr0, s_next, cols24);
@@ -963,6 +1047,7 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
     // A body with an event due: checked, then the tracebacks it raised.
     {
       uint32_t Pw[kPw];
+      publish();
       pwords(Pw, base);
       pk.ring = ring_block + slot * kSlotBytes;
       pk.template body<true, 0>(M, Pw, tr0, s_next, cols24);
@@ -981,6 +1066,7 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
     // A deferred traceback walk runs in the next body's columns (checked: rare).
     if (W.we && __builtin_amdgcn_ballot_w64(R.live) != 0) {
       uint32_t Pw[kPw];
+      publish();
       pwords(Pw, base);
       pk.ring = ring_block + slot * kSlotBytes;
       if (W.we == 3) pk.template body<true, 3>(M, Pw, tr0, s_next, cols24);
@@ -992,6 +1078,12 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
       }
       if constexpr ((DBG & 1) != 0) R.ppend = R.fpend = false;
       next_body();
+    }
+  }
+  if constexpr (kPrioMode >= 2) {
+    if (prio) {                                        // leaving: no columns left
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_raw_buffer_store_b32(0u, prs, (int)(4u * wid), 0, kSc0);
     }
   }
   if (W.we) walk_finish(W, ring_block, rib * 64u);     // rows done before the deferred tail ran
@@ -1139,6 +1231,11 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
           for (int d = 0; d < v3::kDw; d++)
             M[d] = ((v3::pos_of(l, d, 1) ? 48u : 0u) << 24) | ((v3::pos_of(l, d, 0) ? 48u : 0u) << 8);
         }
+        // issue priority (run_rows): longest remaining first for a mixed batch's rows, the
+        // younger wave's 2 of 3 bodies otherwise
+        const bool mixed = rows != nullptr && uni == 0u;
+        const bool lrpt = !FIX && (v3::kPrioMode == 2 || (v3::kPrioMode == 3 && mixed));
+        const bool younger = !FIX && (v3::kPrioMode == 1 || (v3::kPrioMode == 3 && !mixed)) && ((blockIdx.x / ncu) & 1u) != 0u;
         v3::Row Rr;
         Rr.ob = xfix ? v3::kSegWarm - v3::kSegCmp : xk ? v3::kSegWarm : 0u;
         Rr.end = x.E - x.S; Rr.cols = colsS;
@@ -1150,9 +1247,9 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
         for (int d = 0; d < v3::kDw; d++) Rr.pM[d] = Rr.fM[d] = 0u;
         Rr.nbytes = 0;
         Rr.next = v3::row_next(Rr);
-        if (rate == 0) v3::run_rows<0, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M, rowx, dumps, !FIX && ((blockIdx.x / ncu) & 1u) != 0u);
-        else if (rate == 1) v3::run_rows<1, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M, rowx, dumps, !FIX && ((blockIdx.x / ncu) & 1u) != 0u);
-        else v3::run_rows<2, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M, rowx, dumps, !FIX && ((blockIdx.x / ncu) & 1u) != 0u);
+        if (rate == 0) v3::run_rows<0, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M, rowx, dumps, lrpt, younger);
+        else if (rate == 1) v3::run_rows<1, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M, rowx, dumps, lrpt, younger);
+        else v3::run_rows<2, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M, rowx, dumps, lrpt, younger);
         if (mq) nbytes = Rr.nbytes;
       }
     }
