@@ -1,5 +1,6 @@
 #!/bin/bash
-# Config 5: more than two block rounds with the blocks in plain longest-first dispatch order
+# Config 5: more than two block rounds with the blocks in plain longest-first dispatch order (the
+# ZRX_RANK_LPT switch of commit "rank_place: ZRX_RANK_LPT A/B switch", since removed: re-add it to rerun)
 # (ZRX_RANK_LPT) at segment cuts of 8/8, 9/8, 10/8, 11/8 L, against the in-tree build.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out

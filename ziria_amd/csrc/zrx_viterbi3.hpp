@@ -334,9 +334,6 @@ __host__ __device__ __forceinline__ uint32_t order_place(uint32_t pos, uint32_t 
 // alone on the CUs the second round leaves free (the shortest of them on the CU that also
 // gets the partial last block, slot nfull), the rest paired longest with shortest.  More
 // rounds: the snake of order_place over the ranks.  A permutation of 0 .. nfull - 1.
-#ifndef ZRX_RANK_LPT
-#define ZRX_RANK_LPT 0
-#endif
 constexpr int kRankBlocks = 4096;                      // ranked when the batch has at most this many
 __host__ __device__ __forceinline__ uint32_t rank_place(uint32_t r, uint32_t nfull, uint32_t ncu, uint32_t rcp) {
   if (nfull <= ncu) return r;
@@ -346,11 +343,7 @@ __host__ __device__ __forceinline__ uint32_t rank_place(uint32_t r, uint32_t nfu
     const uint32_t q = r - alone;                      // CU c: ranks alone + c and alone + 2 n2 - 1 - c
     return q < n2 ? q : ncu + (2u * n2 - 1u - q);
   }
-#if ZRX_RANK_LPT
-  return r;                                            // (A/B: longest first in dispatch order)
-#else
   return order_place(r * (uint32_t)kRows, nfull, ncu, rcp) / (uint32_t)kRows;
-#endif
 }
 // The plan header k_pkt_plan writes for k_viterbi3 (int32 words of the nrows buffer).
 enum PlanWord { kPlanRows = 0, kPlanFixes = 1, kPlanUniform = 2, kPlanNcu = 3, kPlanSegLen = 4, kPlanDropped = 5 };   // (8 words)
