@@ -44,6 +44,10 @@ VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # 256 CU x 4 SIMD x 32 lanes/clk 
 HBM_PEAK_GBS = 8000.0
 OPS_PER_DECODED_BIT = 256                       # 64 ACS x (add, add, compare, select)
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
+# Two rx batches in flight pay only while one batch's Viterbi leaves the GPU idle around it:
+# interleaved on one box (profiles/r04_pipeline_probe.txt, Gbit/s, one engine / two linked):
+# 2048 packets 101.5 / 114.6, 4096 125.2 / 133.3, 8192 140.7 / 131.6, 16384 155.3 / 155.1.
+PIPELINE_BELOW = 8192
 
 
 def traffic_for(kernel, npkts):
@@ -70,9 +74,11 @@ def main():
     ap.add_argument("--payload", type=int, default=1500)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall time budget of the CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--pipeline", type=int, default=2, choices=[1, 2],
+    ap.add_argument("--pipeline", type=int, default=0, choices=[0, 1, 2],
                     help="batches in flight: 2 = two engines (own workspace and stream) take the steps in "
-                         "turn, as a streaming receiver would, so one batch's tail overlaps the next one's head")
+                         "turn, as a streaming receiver would, so one batch's tail overlaps the next one's head; "
+                         "0 (default) = auto: 2 for an rx batch under %d packets per GPU (zrx_pipeline_link "
+                         "mode 1) and for configs 2 and 5, else 1" % PIPELINE_BELOW)
     ap.add_argument("--batches", type=int, default=2,
                     help="distinct input batches per GPU the steps rotate through (config 3/4/5)")
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 5])
@@ -113,10 +119,16 @@ def main():
     total = args.total if args.total else args.npkts * world
     sigma = 2.0 if args.eq else 4.0
     nb = args.batches
-    # args.pipeline engines, each with its own workspace and stream, take the steps in turn;
-    # every step is still one whole pass of the chain over one batch
-    engs = [RxEngine(local) for _ in range(args.pipeline)]
-    streams = [torch.cuda.Stream(dev) for _ in range(args.pipeline)]
+    lo, hi = node.shard_range(total, world, rank)
+    npipe = args.pipeline or (2 if hi - lo < PIPELINE_BELOW else 1)
+    # npipe engines, each with its own workspace and stream, take the steps in turn; every
+    # step is still one whole pass of the chain over one batch.  Two engines are linked
+    # (zrx_pipeline_link mode 1): one batch's Viterbi starts only once the other batch's chain
+    # is done, so only the short kernels around it overlap.
+    engs = [RxEngine(local) for _ in range(npipe)]
+    streams = [torch.cuda.Stream(dev) for _ in range(npipe)]
+    if npipe == 2:
+        engs[0].link(engs[1], 1)
     eng = engs[0]
     state = {}
 
@@ -176,6 +188,8 @@ def main():
                            on_timed=instrumented, nbatches=nb)
     stage = state["stage"]
     n, S = res["hi"] - res["lo"], state["S"]
+    for e in engs:                                         # the Viterbi plans dropped no rows (ZRX_EPLAN)
+        e.plan_check()
     elapsed = res["elapsed"]
 
     # the same K steps with engine 0 alone (one batch in flight): the pipelined value above is
@@ -230,7 +244,9 @@ def main():
                        "packets_total": total, "packets_per_gpu": n, "payload_bytes": args.payload,
                        "symbols_per_packet": S, "parallelism": f"packet-sharded x{world}",
                        "batches_per_gpu": nb,
-                       "pipeline": f"{len(engs)} batches in flight (engines on separate streams, steps in turn)"},
+                       "pipeline": f"{len(engs)} batch{'es' if len(engs) > 1 else ''} in flight"
+                                   + (" (engines on separate streams, steps in turn, linked: a Viterbi starts after "
+                                      "the other batch's chain)" if len(engs) > 1 else "")},
             "value_one_engine": round(res["bits"] * args.steps / single / 1e6, 1),
             "bit_exact_check": {"crc_pass": res["ok"], "packets": res["packets"],
                                 "payload_match": res["payload_match"],
@@ -320,7 +336,7 @@ def bench_viterbi_only(args):
     soft_off = torch.arange(n, dtype=torch.int64, device=dev) * ns
     params = torch.tensor([fl, 0, ns, 0], dtype=torch.int32, device=dev).repeat(n, 1).contiguous()
     out_off = torch.arange(n, dtype=torch.int64, device=dev) * stride
-    engs = [RxEngine(0) for _ in range(args.pipeline)]
+    engs = [RxEngine(0) for _ in range(args.pipeline or 2)]
     streams = [torch.cuda.Stream(dev) for _ in engs]
     outs = []
     for e in engs:
@@ -394,8 +410,8 @@ def bench_mixed(args):
           for j in range(nb)]
     gen_s = time.perf_counter() - tg
     S = max(m["max_nsym"] for m in ms)
-    # args.pipeline engines (own workspace and stream) take the steps in turn, as in main()
-    engs = [RxEngine(0) for _ in range(args.pipeline)]
+    # args.pipeline engines (own workspace and stream; auto: 2) take the steps in turn, as in main()
+    engs = [RxEngine(0) for _ in range(args.pipeline or 2)]
     streams = [torch.cuda.Stream(dev) for _ in engs]
     outs = []
     for e in engs:

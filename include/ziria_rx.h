@@ -170,6 +170,13 @@ int zrx_enable_timing(zrx_ctx* ctx, int on);
  * if nothing was recorded. */
 int zrx_get_timing(zrx_ctx* ctx, float* ms5);
 
+/* Two contexts taking a stream of rx batches in turn (two batches in flight, each on its own
+ * stream).  mode 0 unlinks them; with bit 0 set a context's data Viterbi waits until the
+ * peer's last launched chain has finished (so the Viterbi grid is always placed on an
+ * otherwise idle GPU); with bit 1 its data FFT waits until the peer's last launched data
+ * Viterbi has finished.  Event waits only: results never change. */
+int zrx_pipeline_link(zrx_ctx* a, zrx_ctx* b, int mode);
+
 /* d_in/d_out: 64*nsym complex16 each (may alias). */
 int zrx_fft64_dev(zrx_ctx* ctx, const struct complex16* d_in, struct complex16* d_out, int64_t nsym);
 /* FFTSafe<nfft> (csrc/fft_r4difx.hpp:220-237) of count consecutive blocks of nfft complex16

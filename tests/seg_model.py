@@ -13,7 +13,7 @@ Geometry (same formulas as v3::seg_start / seg_count / seg_stop):
 """
 import numpy as np
 
-UNIT, WARM, CMP, MAX_SEG, MIN_SEG, MAX_END = 768, 256, 240, 8, 1536, 1 << 24
+UNIT, WARM, CMP, MAX_SEG, MIN_SEG, MIN_CUT, MAX_END = 768, 256, 240, 8, 1536, 1024, 1 << 24
 PREFIX, LOOK, DEPTH = 6, 24, 256
 
 _S = np.arange(64)
@@ -45,11 +45,12 @@ def seg_start(E, nseg, k):
     return 0 if k == 0 else UNIT * ((2 * k * E + nseg * UNIT) // (2 * nseg * UNIT))
 
 
-def seg_count(E, cols, L):
-    if cols < E or E > MAX_END or E < 2 * MIN_SEG or L == 0:
+def seg_count(E, cols, L, min_len=MIN_SEG):
+    """v3::seg_count: min_len MIN_SEG for a mixed batch, MIN_CUT for a uniform one."""
+    if cols < E or E > MAX_END or E < 2 * min_len or L == 0:
         return 1
     n = (cols + L - 1) // L
-    n = min(n, E // MIN_SEG)
+    n = min(n, E // min_len)
     return min(max(n, 1), MAX_SEG)
 
 

@@ -53,6 +53,10 @@ HARNESS = textwrap.dedent("""
             log.append(("new", self.id))
         def reserve(self, n, s):
             pass
+        def link(self, other, mode):
+            log.append(("link", self.id, other.id, mode))
+        def plan_check(self):
+            log.append(("plan_check", self.id))
         def enable_timing(self, on):
             log.append(("timing", on))
         def stage_ms(self):
@@ -129,6 +133,7 @@ def test_bench_pipelined_flow(oracle, tmp_path, args, k, w):
     assert [e[1:] for e in timed] == [[(w + i) % 2, (w + i) % nb] for i in range(k)]
     assert [e[1:] for e in verify] == [[j, bi] for bi in range(nb) for j in range(2)]
     if "--config" not in args:                      # config 3: the single-engine pass, K steps on engine 0
+        assert ["link", 0, 1, 1] in log and ["plan_check", 0] in log and ["plan_check", 1] in log
         single = rest[k + 2 * nb:]                  # its own warmup, then the K timed steps
         assert [e[1:] for e in single] == [[0, i % nb] for i in range(w)] + [[0, i % nb] for i in range(k)]
         assert line["config"]["batches_per_gpu"] == nb and b["packets"] == nb * 24
@@ -161,3 +166,13 @@ def test_bench_gpus2_spawns_two_ranks(oracle, tmp_path):
     assert line["cpu_baseline"]["value"] > 0
     for r in (0, 1):
         assert any(e[0] == "rx" for e in logs[r])
+
+
+def test_bench_one_engine_flow(oracle, tmp_path):
+    """--pipeline 1 (auto's choice at 8192 packets per GPU and above): one engine, no link,
+    the timed steps and the verification all on engine 0."""
+    line, logs = _run(tmp_path, ["--npkts", "24", "--steps", "3", "--warmup", "1", "--no-cpu", "--pipeline", "1"])
+    log = logs[0]
+    assert "1 batch in flight" in line["config"]["pipeline"]
+    assert not any(e[0] == "link" for e in log) and all(e[1] == 0 for e in log if e[0] == "rx")
+    assert line["bit_exact_check"]["payload_match"] is True and line["value_one_engine"] > 0

@@ -71,3 +71,30 @@ def test_batch_mode_receiver_kats(hooked, tmp_path, golden):
                       f"--output-file-name={out}", "--output-file-mode=dbg"] + extra)
         got = _vals(out.read_text()).astype(np.int8).view(np.uint8)
         assert (got == fe[f"{tag}_out"]).all(), tag
+
+
+def test_program_binds_library_fft(hooked, tmp_path, golden):
+    """The FFT half of the drop-in: the stub program is compiled as wplc output is (through
+    csrc/common.h, which #includes sora_ext_lib.cpp), with integration/csrc/sora_ext_lib.cpp.patch
+    and -DZIRIA_HIP_EXT, so __ext_sora_fft and __ext_sora_fft_dynamic are undefined in the
+    executable and bind to libziria_rx.so; run through the reference driver's stream path, the
+    program's FFT of the tests/libs/test_fft KAT and of the 42-size KAT equals the ground."""
+    nm = subprocess.check_output(["nm", hooked]).decode()
+    for sym in ("_Z14__ext_sora_fftP9complex16iS0_i", "_Z22__ext_sora_fft_dynamicP9complex16isS0_i"):
+        assert any(ln.split()[-2:] == ["U", sym] for ln in nm.splitlines()), sym
+    kat = golden["ref_kats"]
+    fn = golden["ref_fftn"]
+    cases = [(64, kat["fft64_kat_in"], kat["fft64_kat_out"])]
+    off = 0
+    for n in fn["sizes"]:
+        cases.append((int(n), fn["kat_in"][off:off + n], fn["kat_out"][off:off + n]))
+        off += int(n)
+    assert off == fn["kat_in"].shape[0]
+    for n, x, y in cases:
+        src, dst = tmp_path / f"in{n}.bin", tmp_path / f"out{n}.bin"
+        np.asarray(x, "<i2").tofile(src)
+        env = dict(os.environ, ZRX_STUB_FFT_IN=str(src), ZRX_STUB_FFT_OUT=str(dst), ZRX_STUB_FFT_N=str(n))
+        r = subprocess.run([hooked, "--input=dummy", "--output=dummy", "--dummy-samples=10"], env=env,
+                           capture_output=True, text=True, timeout=60)
+        assert r.returncode == 0, (n, r.returncode, r.stderr[-500:])
+        assert (np.fromfile(dst, "<i2").reshape(-1, 2) == y).all(), n

@@ -129,3 +129,31 @@ def test_segments_uniform_batch_with_fixes(oracle):
     for i, (s, _, _) in enumerate(frames):
         exp = oracle.viterbi_decode(s, fl, cr)
         assert bits[i] == 8 * fl and (got[i] == exp).all(), i
+
+
+def test_segments_small_uniform_batch_min_cut(oracle):
+    """A small uniform batch is cut down to kMinCut-column segments (v3::seg_count with
+    kMinCut): 600-byte frames (E = 4806) take 4 segments starting at units 0, 2, 3, 5, so one
+    segment spans a single 768-column unit.  Half the frames are pure noise (seams disagree,
+    the fix pass runs); every frame equals the oracle."""
+    fl, cr = 600, 1
+    frames = [(synth.viterbi_soft(cr, fl, -1 if i % 2 else 2, seed=4100 + i), fl, cr) for i in range(128)]
+    got, bits, (rows, fixes) = _run(frames)
+    assert rows == 128 * 4 and fixes > 0
+    for i, (s, _, _) in enumerate(frames):
+        exp = oracle.viterbi_decode(s, fl, cr)
+        assert bits[i] == 8 * fl and (got[i] == exp).all(), i
+
+
+def test_segments_config4_shard(oracle):
+    """The per-GPU Viterbi of config 4 at N = 8 (2048 frames of 1504 B at rate 3/4, a config-3
+    shard): 8 segments per frame, i.e. 16384 rows (two waves per SIMD); 16 distinct frames
+    tiled, each equal to the oracle."""
+    fl, cr = 1504, 2
+    base = [(synth.viterbi_soft(cr, fl, 3, seed=4300 + i), fl, cr) for i in range(16)]
+    got, bits, (rows, fixes) = _run(base * 128)
+    assert rows == 2048 * 8 and fixes == 0
+    exp = [oracle.viterbi_decode(s, fl, cr) for s, _, _ in base]
+    assert (bits == 8 * fl).all()
+    for i, g in enumerate(got):
+        assert (g == exp[i % 16]).all(), i

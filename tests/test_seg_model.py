@@ -15,7 +15,7 @@ def test_geometry_invariants():
         for cr in (0, 1, 2):
             K = (24, 32, 36)[cr]                             # decoded bits per 48 soft values
             cols = -(-E // K) * K
-            for nseg in range(2, min(SM.MAX_SEG, E // SM.MIN_SEG) + 1):
+            for nseg in range(2, min(SM.MAX_SEG, E // SM.MIN_CUT) + 1):
                 S = [SM.seg_start(E, nseg, k) for k in range(nseg)]
                 assert S[0] == 0 and all(b > a for a, b in zip(S, S[1:]))
                 for k in range(1, nseg):
@@ -27,8 +27,9 @@ def test_geometry_invariants():
 
 
 def test_row_bound():
-    """sum of segments <= batch columns / L' + packets, L' = 9/8 L (uniform batch) or 11/8 L
-    (mixed, v3::kSegMixNum), L = max(1536, columns / (64 ncu)): within the grid of k_viterbi3's
+    """sum of segments <= batch columns / L' + packets, L' = 9/8 max(1024, columns / (64 ncu))
+    (uniform batch) or 11/8 L (mixed, v3::kSegMixNum), L = max(1536, columns / (64 ncu)): within
+    the grid of k_viterbi3's
     planned launch (zrx_api.hip plan_rows_max), for mixed and uniform batches."""
     rng = np.random.default_rng(3)
     ncu, mix = 256, 11
@@ -43,9 +44,11 @@ def test_row_bound():
             cols = 8 * fl + 6 + rng.integers(0, 300, n)
         E = 8 * fl + 6
         T = int(np.sum(cols))
-        L = max(SM.MIN_SEG, -(-T // (64 * ncu)))
-        Lq = L + L // 8 if it % 2 else max(L * mix // 8, SM.MIN_SEG)
-        rows = sum(SM.seg_count(int(e), int(c), Lq) for e, c in zip(E, np.broadcast_to(cols, E.shape)))
+        L0 = -(-T // (64 * ncu))
+        L, Lu = max(SM.MIN_SEG, L0), max(SM.MIN_CUT, L0)
+        Lq = Lu + Lu // 8 if it % 2 else max(L * mix // 8, SM.MIN_SEG)
+        mn = SM.MIN_CUT if it % 2 else SM.MIN_SEG
+        rows = sum(SM.seg_count(int(e), int(c), Lq, mn) for e, c in zip(E, np.broadcast_to(cols, E.shape)))
         assert rows <= min(n + r + r // 256 + 64, n * SM.MAX_SEG), (it, n, rows)
 
 
@@ -74,7 +77,8 @@ def test_rank_place():
 
 
 CASES = [(cr, fl, noise, nseg) for cr in (0, 1, 2) for fl, noise, nseg in
-         [(400, 0, 2), (700, 3, 3), (1100, 2, 5), (700, -1, 3), (1100, -1, 5)]]
+         [(400, 0, 2), (700, 3, 3), (1100, 2, 5), (700, -1, 3), (1100, -1, 5),
+          (500, 2, 3), (500, -1, 3)]]      # (500: E / 3 = 1335 >= kMinCut, a one-unit middle segment)
 
 
 @pytest.mark.parametrize("cr,fl,noise,nseg", CASES)

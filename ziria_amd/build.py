@@ -80,7 +80,7 @@ def build(force=False, verbose=False):
     objs = []
     for src in HOST_SRCS:
         obj = os.path.join(LIBDIR, os.path.splitext(src)[0] + ".o")
-        cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-mavx2", "-Wall", "-Wextra", "-c", "-o", obj,
+        cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wextra", "-c", "-o", obj,
                os.path.join(CSRC, src)]
         if verbose:
             print(" ".join(cmd))

@@ -95,6 +95,10 @@ struct zrx_ctx {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int32_t* mixed_hint = nullptr;  // pinned, mapped: 1 when the last planned batch was mixed
   int32_t* mixed_hint_dev = nullptr;
+  // zrx_pipeline_link: the context taking the other half of a stream of batches
+  zrx_ctx* peer = nullptr;
+  int link_mode = 0;
+  hipEvent_t ev_vit_done = nullptr, ev_chain_done = nullptr;   // recorded every chain while linked
 };
 
 static int check_device(int device) {
@@ -460,6 +464,9 @@ int zrx_destroy(zrx_ctx* c) {
   for (auto& set : c->evsets)
     for (auto& e : set) (void)hipEventDestroy(e);
   if (c->ws_free) (void)hipEventDestroy(c->ws_free);
+  if (c->peer) { c->peer->peer = nullptr; c->peer->link_mode = 0; }
+  if (c->ev_vit_done) (void)hipEventDestroy(c->ev_vit_done);
+  if (c->ev_chain_done) (void)hipEventDestroy(c->ev_chain_done);
   if (c->side) {
     (void)hipStreamDestroy(c->side);
     (void)hipEventDestroy(c->ev_fork);
@@ -472,6 +479,22 @@ int zrx_destroy(zrx_ctx* c) {
 int zrx_set_stream(zrx_ctx* c, void* stream) {
   if (!c) return ZRX_EINVAL;
   c->stream = (hipStream_t)stream;
+  return ZRX_OK;
+}
+
+int zrx_pipeline_link(zrx_ctx* a, zrx_ctx* b, int mode) {
+  if (!a || !b || a == b || mode < 0 || mode > 3) return ZRX_EINVAL;
+  for (zrx_ctx* c : {a, b}) {
+    if (c->peer && c->peer != a && c->peer != b) { c->peer->peer = nullptr; c->peer->link_mode = 0; }
+    // stream-to-stream on one device: no system-scope fence (which writes back the L2s)
+    if (!c->ev_vit_done)
+      ZRX_CHECK(hipEventCreateWithFlags(&c->ev_vit_done, hipEventDisableTiming | hipEventDisableSystemFence));
+    if (!c->ev_chain_done)
+      ZRX_CHECK(hipEventCreateWithFlags(&c->ev_chain_done, hipEventDisableTiming | hipEventDisableSystemFence));
+  }
+  a->peer = mode ? b : nullptr;
+  b->peer = mode ? a : nullptr;
+  a->link_mode = b->link_mode = mode;
   return ZRX_OK;
 }
 
@@ -679,6 +702,9 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
   // k_data_fft: waves over the batch's data symbols, at most npkts x (max_nsym - 1) of them
   const int fft_blocks = (int)std::min<int64_t>(((int64_t)npkts * (max_nsym - 1) + 255) / 256,
                                                 (int64_t)(chan ? c->df_blocks_eq : c->df_blocks));
+  zrx_ctx* const peer = c->peer;
+  // (a never-recorded peer event is complete: the first batch waits for nothing)
+  if (peer && (c->link_mode & 2)) ZRX_CHECK(hipStreamWaitEvent(s, peer->ev_vit_done, 0));
   if (fft_blocks > 0) {
     if (chan)
       k_data_fft<true><<<fft_blocks, 256, 0, s>>>((const uint4*)d_sym, d_sym_off, c->vparams, npkts, (uint4*)c->soft,
@@ -689,11 +715,14 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
   }
   if (ev) ZRX_CHECK(hipEventRecord(ev[3], s));
   if (split) ZRX_CHECK(hipStreamWaitEvent(s, c->ev_join, 0));
+  if (peer && (c->link_mode & 1)) ZRX_CHECK(hipStreamWaitEvent(s, peer->ev_chain_done, 0));
   launch_viterbi(c, c->soft, c->soft_off, c->vparams, npkts, c->dec, c->dec_off, c->dec_bits, ordered);
+  if (peer) ZRX_CHECK(hipEventRecord(c->ev_vit_done, s));
   if (ev) ZRX_CHECK(hipEventRecord(ev[4], s));
   k_descramble_crc<<<c->crc_blocks > 0 ? std::min(blocks(npkts, kCrcWaves), c->crc_blocks) : blocks(npkts, kCrcWaves),
                      64 * kCrcWaves, 0, s>>>(c->dec, c->dec_bits, d_info, d_payload, npkts);
   if (ev) ZRX_CHECK(hipEventRecord(ev[5], s));
+  if (peer) ZRX_CHECK(hipEventRecord(c->ev_chain_done, s));
   ZRX_CHECK(hipGetLastError());
   return ws_release(c);
 }
@@ -925,7 +954,8 @@ int32_t viterbi_batch_decode(const char* soft, int softlen, const int32_t* pkt_s
   if (rc) return rc;
   ZRX_CHECK(hipMemcpyAsync(out_bits, d_out, (size_t)out_bytes, hipMemcpyDeviceToHost, c->stream));
   ZRX_CHECK(hipStreamSynchronize(c->stream));
-  return np;
+  rc = zrx_plan_check(c);                            // rows dropped by the plan: ZRX_EPLAN, never silent
+  return rc ? rc : np;
 }
 
 
@@ -975,6 +1005,8 @@ int32_t wifi_rx_batch(struct complex16* sym, int nsym_total, const int32_t* pkt_
   ZRX_CHECK(hipMemcpyAsync(payload, d_pay, s_pay, hipMemcpyDeviceToHost, c->stream));
   ZRX_CHECK(hipMemcpyAsync(pkt_info, d_info, s_info, hipMemcpyDeviceToHost, c->stream));
   ZRX_CHECK(hipStreamSynchronize(c->stream));
+  rc = zrx_plan_check(c);                            // rows dropped by the plan: ZRX_EPLAN, never silent
+  if (rc) return rc;
   int ok = 0;
   for (int i = 0; i < np; i++) ok += pkt_info[8 * i + 4] != 0;
   return ok;
@@ -1023,6 +1055,8 @@ int32_t wifi_rx_stream_batch(struct complex16* samples, int nsamples, const int3
   ZRX_CHECK(hipMemcpyAsync(pkt_info, d_info, (size_t)nc * 32, hipMemcpyDeviceToHost, c->stream));
   ZRX_CHECK(hipMemcpyAsync(det, d_det, s_det, hipMemcpyDeviceToHost, c->stream));
   ZRX_CHECK(hipStreamSynchronize(c->stream));
+  rc = zrx_plan_check(c);                            // rows dropped by the plan: ZRX_EPLAN, never silent
+  if (rc) return rc;
   int ok = 0;
   for (int i = 0; i < nc; i++) ok += det[fe::kDetWords * i] && pkt_info[8 * i + 4] != 0;
   return ok;

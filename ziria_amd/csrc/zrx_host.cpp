@@ -5,7 +5,9 @@
 // next call, so a GPU launch + sync per call (10-65 us) cannot compete with a host core; the
 // batched externals (zrx_api.hip) are where the GPU decodes.
 //
-// Compiled with -mavx2 (x86-64 hosts of MI355X nodes all have it; checked at first use).
+// The SIMD functions carry __attribute__((target("avx2"))); the file is compiled without
+// -mavx2, so nothing else (static initializers, the plan code) uses AVX2 and require_avx2()
+// can report a host without it before any AVX2 instruction runs.
 //   FFT      FFTSafe<N> (csrc/fft_r4difx.hpp:220-237, csrc/sora_ext_lib.cpp:2672-2812) for every
 //            size, executing the plans of zrx_fftplan.hpp with the SSE bricks' integer
 //            semantics; FFT64 (the WiFi symbol) has a dedicated AVX2 path.
@@ -182,6 +184,22 @@ struct Fft64Tables {
   }
 };
 
+// twiddle registers of the 64- and 16-point stages (functors, not lambdas: a lambda does not
+// inherit the enclosing function's target("avx2"))
+struct Tw64 {
+  const Fft64Tables* T;
+  int h;
+  __attribute__((target("avx2"))) __m256i operator()(int k, int j) const {
+    return _mm256_load_si256((const __m256i*)&T->t64[k - 1][j][16 * h]);
+  }
+};
+struct Tw16 {
+  const Fft64Tables* T;
+  __attribute__((target("avx2"))) __m256i operator()(int k, int j) const {
+    return _mm256_load_si256((const __m256i*)&T->t16[k - 1][j][0]);
+  }
+};
+
 // The radix-4 butterfly on registers a, b, c, d (quarter rows), twiddles from tab[k-1][0/1]
 template <class Tw>
 __attribute__((target("avx2"))) inline void r4_v(__m256i& a, __m256i& b, __m256i& c, __m256i& d, Tw tw) {
@@ -217,8 +235,7 @@ __attribute__((target("avx2"))) void fft64_avx2(const c16* in, c16* out) {
   for (int i = 0; i < 8; i++) v[i] = _mm256_loadu_si256((const __m256i*)(in + 8 * i));
   // stage 64: butterfly n over x[n], x[n+16], x[n+32], x[n+48]: registers (i, i+2, i+4, i+6)
   for (int h = 0; h < 2; h++) {
-    auto tw = [h](int k, int j) { return _mm256_load_si256((const __m256i*)&T.t64[k - 1][j][16 * h]); };
-    r4_v(v[h], v[h + 2], v[h + 4], v[h + 6], tw);
+    r4_v(v[h], v[h + 2], v[h + 4], v[h + 6], Tw64{&T, h});
   }
   // stage 16 on each 16-block q (registers 2q, 2q+1): n over x[16q + n + 4r], r = 0..3; with
   // 8 complex per register, quarters r = 0,1 sit in register 2q (halves), r = 2,3 in 2q+1.
@@ -230,8 +247,7 @@ __attribute__((target("avx2"))) void fft64_avx2(const c16* in, c16* out) {
     __m256i b = _mm256_permute2x128_si256(u0, u2, 0x31);   // r1
     __m256i c = _mm256_permute2x128_si256(u1, u3, 0x20);   // r2
     __m256i d = _mm256_permute2x128_si256(u1, u3, 0x31);   // r3
-    auto tw = [](int k, int j) { return _mm256_load_si256((const __m256i*)&T.t16[k - 1][j][0]); };
-    r4_v(a, b, c, d, tw);
+    r4_v(a, b, c, d, Tw16{&T});
     v[4 * p] = _mm256_permute2x128_si256(a, b, 0x20);
     v[4 * p + 1] = _mm256_permute2x128_si256(c, d, 0x20);
     v[4 * p + 2] = _mm256_permute2x128_si256(a, b, 0x31);

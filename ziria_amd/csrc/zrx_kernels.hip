@@ -476,16 +476,18 @@ __global__ __launch_bounds__(1024) void k_pkt_plan(const int32_t* __restrict__ v
   if (!same) uniform = 0;
   __syncthreads();
   const uint64_t rt = 64ull * (uint64_t)max(ncu, 1);   // rows that give every SIMD four waves
-  const uint32_t L = (uint32_t)min<uint64_t>(max<uint64_t>((tcols + rt - 1) / rt, v3::kMinSeg), 0xFFFFFFFFull);
+  const uint32_t L0 = (uint32_t)min<uint64_t>((tcols + rt - 1) / rt, 0xFFFFFFFFull);
+  const uint32_t L = max(L0, v3::kMinSeg);
   // (a frame is cut only when it is more than L + L / 8 long: a batch of equal frames just
-  // short of four waves per SIMD stays whole)
-  const uint32_t Lb = L + L / 8u;                       // (uniform batch)
+  // short of four waves per SIMD stays whole; a small uniform batch down to kMinCut)
+  const uint32_t Lu = max(L0, v3::kMinCut);
+  const uint32_t Lb = Lu + Lu / 8u;                     // (uniform batch)
   const uint32_t Lm = max(L * v3::kSegMixNum / 8u, v3::kMinSeg);   // (mixed batch)
   if (t == 0 && mixed_hint) *mixed_hint = uniform ? 0 : 1;   // (host-mapped: the next call's split choice)
   if (uniform) {                                       // no sort: k_viterbi3 derives each row's segment
     if (t == 0) {
       const uint32_t E0 = q0.x > (1 << 21) ? 0xFFFFFFFFu : (uint32_t)q0.x * 8u + 6u;
-      const uint32_t n0 = v3::seg_count(E0, cols_of(q0.y, q0.z), Lb);
+      const uint32_t n0 = v3::seg_count(E0, cols_of(q0.y, q0.z), Lb, v3::kMinCut);
       nrows[v3::kPlanRows] = (int32_t)min((uint32_t)npkts * n0, (uint32_t)rows_cap);
       nrows[v3::kPlanFixes] = 0;
       nrows[v3::kPlanUniform] = (int32_t)n0;

@@ -293,7 +293,12 @@ constexpr uint32_t kSegUnit = 768;
 constexpr uint32_t kSegWarm = 256;                     // S_k -> J_k
 constexpr uint32_t kSegCmp = 240;                      // S_k -> C_k
 constexpr int kMaxSeg = 8;
-constexpr uint32_t kMinSeg = 1536;                     // columns per segment at least
+constexpr uint32_t kMinSeg = 1536;                     // columns per segment at least (mixed batch)
+// A uniform batch too small to give every SIMD two waves of whole frames is cut into segments
+// of at least kMinCut columns: a 2048-packet config-3 shard (a config-4 rank at N = 8) then
+// takes 8 segments of 2 units (16384 rows, two waves per SIMD) instead of 7 of 2-3 units,
+// whose longest row (3 units + the seam overlap) set the kernel's time.
+constexpr uint32_t kMinCut = 1024;
 constexpr uint32_t kSegMaxEnd = 1u << 24;              // longer frames are not split
 constexpr uint32_t kSeamWords = 32;                    // uint2 per dump slot (kLanes x kDw / 2 used: 16)
 // Segment length of a mixed batch: L x kSegMixNum / 8, L = the batch's columns / (64 rows
@@ -349,16 +354,19 @@ __host__ __device__ __forceinline__ uint32_t rank_place(uint32_t r, uint32_t nfu
 enum PlanWord { kPlanRows = 0, kPlanFixes = 1, kPlanUniform = 2, kPlanNcu = 3, kPlanSegLen = 4, kPlanDropped = 5 };   // (8 words)
 
 // start unit m_k of segment k >= 1 of nseg over a frame of E = 8 len + 6 columns (rounded
-// k E / nseg; with E / nseg >= kMinSeg the m_k are distinct and S_k + 256 + 64 <= E)
+// k E / nseg; with E / nseg >= kMinCut the m_k are distinct (steps of > 1 unit) and
+// S_k + 256 + 64 <= E (the last start is at most (nseg - 1) E / nseg + 384))
 __host__ __device__ __forceinline__ uint32_t seg_start(uint32_t E, uint32_t nseg, uint32_t k) {
   // floor(x / (1536 nseg)) = floor(floor(x / 1536) / nseg)
   return k == 0 ? 0u : kSegUnit * udiv_small((2u * k * E + nseg * kSegUnit) / (2u * kSegUnit), nseg);
 }
-// segments for a frame of E columns with cols columns of input, target length L
-__host__ __device__ __forceinline__ uint32_t seg_count(uint32_t E, uint32_t cols, uint32_t L) {
-  if (cols < E || E > kSegMaxEnd || E < 2u * kMinSeg || L == 0) return 1u;
+// segments for a frame of E columns with cols columns of input, target length L, segments of
+// at least min_len (kMinSeg or kMinCut) columns
+__host__ __device__ __forceinline__ uint32_t seg_count(uint32_t E, uint32_t cols, uint32_t L,
+                                                       uint32_t min_len = kMinSeg) {
+  if (cols < E || E > kSegMaxEnd || E < 2u * min_len || L == 0) return 1u;
   uint32_t n = (cols + L - 1u) / L;
-  n = min(n, E / kMinSeg);
+  n = min(n, E / min_len);
   return min(max(n, 1u), (uint32_t)kMaxSeg);
 }
 // first column after segment k (absolute): where segment k + 1's first window is written

@@ -67,6 +67,12 @@ class RxEngine:
         """Raises if the last Viterbi plan dropped rows past its workspace bound (ZRX_EPLAN)."""
         check(lib().zrx_plan_check(self._h), "zrx_plan_check")
 
+    def link(self, other, mode):
+        """Two engines taking a stream of batches in turn (zrx_pipeline_link): mode bit 0 =
+        this engine's data Viterbi waits for the other's last launched chain, bit 1 = its data
+        FFT waits for the other's last launched Viterbi; 0 unlinks."""
+        check(lib().zrx_pipeline_link(self._h, other._h, int(mode)), "zrx_pipeline_link")
+
     # ------------------------------------------------------------------ launches
     def fft64(self, sym, out=None):
         """sym: int16 [S, 64, 2] on the device -> FFT64 of every symbol."""
