@@ -8,7 +8,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 TMP=$(mktemp -d)
 trap 'rm -rf "$TMP"' EXIT
 cd "$ROOT/ziria_amd/csrc"
-for f in zrx_host zrx_ext_cxx; do g++ -O3 -std=c++17 -fPIC -mavx2 -c $f.cpp -o "$TMP/$f.o"; done
+for f in zrx_host zrx_ext_cxx; do g++ -O3 -std=c++17 -fPIC -c $f.cpp -o "$TMP/$f.o"; done
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared $FLAGS -o "$ROOT/ziria_amd/_lib/libziria_rx.$NAME.so" \
   zrx_api.hip -x none "$TMP/zrx_host.o" "$TMP/zrx_ext_cxx.o"
 echo "$ROOT/ziria_amd/_lib/libziria_rx.$NAME.so"

@@ -12,7 +12,7 @@ python3 "$TMP/ziria_amd/csrc/gen_tables.py"
 OBJS=""
 for f in zrx_host zrx_ext_cxx; do
   if [ -f "$TMP/ziria_amd/csrc/$f.cpp" ]; then
-    g++ -O3 -std=c++17 -fPIC -mavx2 -c "$TMP/ziria_amd/csrc/$f.cpp" -o "$TMP/$f.o"
+    g++ -O3 -std=c++17 -fPIC -c "$TMP/ziria_amd/csrc/$f.cpp" -o "$TMP/$f.o"
     OBJS="$OBJS $TMP/$f.o"
   fi
 done

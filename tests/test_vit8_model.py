@@ -62,3 +62,33 @@ def test_model_truncated_vs_oracle(oracle):
         exp = oracle.viterbi_decode(s, fl, cr)
         got = V.decode(s, fl, cr)
         assert got.size == exp.size and (got == exp).all()
+
+
+@pytest.mark.parametrize("cr", [0, 1, 2])
+def test_guard_free_columns(golden, oracle, cr):
+    """The guard-free column (zrx_viterbi3.hpp "Guard-free columns"): on the reference frames,
+    the adversarial fixture, noisy and pure-noise frames, no low-half add carries into bit 16
+    (no metric wrap) and the output equals the guarded model's, i.e. the reference's.  Clean
+    and noisy rate-3/4 frames keep every body check's H_min far below the 115 bound; pure
+    noise passes it (the kernel then redoes such bodies with the guard)."""
+    from tests.golden import synth
+    g = golden["ref_viterbi"]
+    cases, so, oo = g["vit_cases"], g["vit_soft_off"], g["vit_out_off"]
+    short = [i for i, c in enumerate(cases) if c[1] <= 333 and c[0] == cr]
+    for i in short[:4]:
+        _, fl, _ = cases[i]
+        st = {}
+        got = V.decode(g["vit_soft"][so[i]:so[i + 1]], int(fl), cr, guard=False, stats=st)
+        assert st["carries"] == 0
+        assert (got == g["vit_out"][oo[i]:oo[i + 1]]).all()
+    st = {}
+    got = V.decode(g["vit_adv_soft"], 1000, cr, guard=False, stats=st)
+    exp = g[f"vit_adv_out_{cr}"]
+    assert st["carries"] == 0 and (got[:exp.size] == exp).all()
+    for noise, seed in ((3, 11), (-1, 12), (-1, 13)):
+        s = synth.viterbi_soft(cr, 300, noise, seed=seed)
+        st = {}
+        got = V.decode(s, 300, cr, guard=False, stats=st)
+        assert st["carries"] == 0 and (got == oracle.viterbi_decode(s, 300, cr)).all()
+        if cr == 2 and noise >= 0:
+            assert st["max_check_hmin"] <= 115

@@ -116,12 +116,17 @@ class Packet(V3.Packet):
         self.out = []
         self.done = False
         self.v5 = True
+        self.guard = True         # False: the guard-free column (zrx_viterbi3.hpp "Guard-free columns")
+        self.carries = 0          # low-half carries into bit 16 (guard-free: must stay 0)
 
     def step5(self, kind, a, b):
         ph = self.tr % 6
         c = self.tr + 1
         k = (c + 1) % 8
-        T = (self.M & (0xFE00FE00 if k == 0 else 0xFFFEFFFF)).astype(np.uint32)
+        if k == 0 or self.guard:
+            T = (self.M & (0xFE00FE00 if k == 0 else 0xFFFEFFFF)).astype(np.uint32)
+        else:
+            T = self.M.copy()
         mk = 2 << k
         P = V3.p_word(kind, a, b)
         BX = np.zeros((NL, ND), np.uint32)
@@ -141,7 +146,9 @@ class Packet(V3.Packet):
         C = ((K + 1) << 8) * 0x00010001 if k == 7 else ((K << 8) | mk) * 0x00010001
         BY = ((C - BX.astype(np.int64)) & 0xFFFFFFFF).astype(np.uint32)
         add = lambda x, y: ((x.astype(np.uint64) + y) & 0xFFFFFFFF).astype(np.uint32)
+        lo_carry = lambda x, y: int((((x.astype(np.uint64) & 0xFFFF) + (y.astype(np.uint64) & 0xFFFF)) > 0xFFFF).sum())
         Tp = partner(T, ph)
+        self.carries += lo_carry(T, BX) + (0 if Tp is None else lo_carry(Tp, BY))
         Z = V3.pk_add(V3.swap_halves(T), BY) if Tp is None else add(Tp, BY)
         X = add(T, BX)
         self.M = V3.pk_min(X, Z)
@@ -186,9 +193,13 @@ class Packet(V3.Packet):
         return [blocks[c] for c in range(c_first, c_hi + 1, 8)]
 
 
-def decode(soft, frame_len, code_rate):
-    """Model of one packet through the 8-lane layout (vit3_model.decode's driver loop)."""
+def decode(soft, frame_len, code_rate, guard=True, stats=None):
+    """Model of one packet through the 8-lane layout (vit3_model.decode's driver loop).
+    guard=False runs the guard-free column everywhere; `stats` (a dict) then receives the
+    low-half carry count (0 whenever no metric wrapped) and the smallest H_min the rate-3/4
+    body checks saw at columns 6, 12, 18 of each 24-column body."""
     P = Packet(frame_len, code_rate)
+    P.guard = guard
     kinds = V3.KINDS[code_rate]
     G = {0: 2, 1: 3, 2: 4}[code_rate]
     soft = np.asarray(soft, np.int64)
@@ -198,6 +209,9 @@ def decode(soft, frame_len, code_rate):
         args = [(s[0], s[1])] + [(v, 0) for v in s[2:]]
         for k, kind in enumerate(kinds):
             P.step5(kind, *args[k])
+            if stats is not None and P.tr % 24 in (6, 12, 18):
+                h = 2 * min(int(((P.M >> 9) & 0x7F).min()), int(((P.M >> 25) & 0x7F).min()))
+                stats["max_check_hmin"] = max(stats.get("max_check_hmin", 0), h)
         if P.tr % 8 == 0:
             P.normalize()
         if P.tr >= P.end:
@@ -218,4 +232,6 @@ def decode(soft, frame_len, code_rate):
             pend = None
     if pend is not None:
         P.out += P.traceback(*pend)
+    if stats is not None:
+        stats["carries"] = stats.get("carries", 0) + P.carries
     return np.array(P.out, np.uint8)

@@ -210,10 +210,12 @@ __device__ __forceinline__ void column_acs(uint32_t (&M)[kDw], const uint32_t (&
   }
   M[D] = w32(__builtin_elementwise_min(h2(X), h2(Z)));
 }
-template <int PH, int KIND, int KPH, int... D>
+// G: clear the carry guard every column.  Without it (G false) the column is AND-free except
+// at KPH 0 (which clears the cycle's history anyway): see "Guard-free columns" below.
+template <int PH, int KIND, int KPH, bool G, int... D>
 __device__ __forceinline__ void column5_(uint32_t (&M)[kDw], uint32_t P, const Consts& K, std::integer_sequence<int, D...>) {
   constexpr uint32_t mask = KPH == 0 ? 0xFE00FE00u : 0xFFFEFFFFu;
-  const uint32_t T[kDw] = {(M[D] & mask)...};
+  const uint32_t T[kDw] = {((KPH == 0 || G) ? (M[D] & mask) : M[D])...};
   constexpr uint32_t mk = 2u << KPH;
   constexpr uint32_t Kc = KIND == 0 ? 28u : 14u;
   constexpr uint32_t C = KPH == 7 ? ((Kc + 1u) << 8) * 0x00010001u : ((Kc << 8) | mk) * 0x00010001u;
@@ -221,9 +223,48 @@ __device__ __forceinline__ void column5_(uint32_t (&M)[kDw], uint32_t P, const C
   (column_bx<PH, KPH, D>(BX, BY, P, K, C), ...);
   (column_acs<PH, D>(M, T, BX, BY), ...);
 }
-template <int PH, int KIND, int KPH>
+template <int PH, int KIND, int KPH, bool G = true>
 __device__ __forceinline__ void column5(uint32_t (&M)[kDw], uint32_t P, const Consts& K) {
-  column5_<PH, KIND, KPH>(M, P, K, std::make_integer_sequence<int, kDw>{});
+  column5_<PH, KIND, KPH, G>(M, P, K, std::make_integer_sequence<int, kDw>{});
+}
+
+// ---- Guard-free columns -------------------------------------------------------------------
+// The guard AND exists for one event: a low half whose H + BM passes 255 (the brick's u8
+// metric wraps) carries into bit 16.  Without wraps there are no carries, and the AND of the
+// columns with KPH 1..7 (84 of the hot body's 96 ANDs at rate 3/4) does nothing.  When can a
+// wrap happen?  H is exact integer arithmetic until the first wrap, bounded by:
+//  * H_min never decreases from column to column (all branch metrics are >= 0) and grows by at
+//    most 14 per full column and 7 per punctured one (a state's two successors differ in both
+//    coded bits, so their branch metrics sum to 28 / 14);
+//  * every state is reached from any state 6 columns earlier (K = 7), so
+//    H_max(t) <= H_min(t - 6) + P6 with P6 the largest branch-metric sum of 6 columns:
+//    168 at rate 1/2, 126 at 2/3 (3 full + 3 punctured), 112 at 3/4 (2 full + 4 punctured);
+//  * normalize subtracts H_min, which is >= H_min 6 columns earlier.
+// Rates 1/2 and 2/3 normalize every 8 columns, so H_min(t - 6) <= 14 in the current
+// normalization's units and H_max + BM <= 14 + 168 + 28 = 210 (the initial 0 / 48 metrics:
+// <= 48 + 5 x 28 + 28 = 216): they never wrap, and run guard-free always.  Rate 3/4
+// normalizes every 24 columns (one body), where the bound allows a wrap late in a body once
+// H_min passes 115.  So a rate-3/4 body runs guard-free speculatively and checks H_min at its
+// columns 6, 12 and 18: if every check finds a state with H <= 115 (a row's H_min <= 115),
+// then for every column t + 1 of the body H_max(t) <= H_min(c) + 112 <= 227 with c the check
+// at or after t - 6 (columns 0..5 use the previous body, H_min <= 0 after its normalize), so
+// no add wrapped (induction over t) and the body is exact.  Otherwise the wave redoes the body
+// from its saved metrics with the guard (config 3 never does: its H stays below 84).  Each
+// check is one 16-bit compare of one half per lane (any state <= 115 suffices) and a ballot.
+#ifndef ZRX_NOGUARD
+#define ZRX_NOGUARD 1
+#endif
+constexpr bool kNoGuard = ZRX_NOGUARD != 0;
+// every row (kLanes-bit group) of a lane mask has a bit set
+__device__ __forceinline__ bool rows_all_any(uint64_t m) {
+  if constexpr (kLanes == 8) {
+    return ((m - 0x0101010101010101ull) & ~m & 0x8080808080808080ull) == 0ull;
+  } else {
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < kRowsWave; r++) ok = ok && ((m >> (r * kLanes)) & kRowMask) != 0ull;
+    return ok;
+  }
 }
 
 // normalize (viterbicore.hpp:149-168): H -= min over the row's 64 H bytes (H even).
@@ -763,9 +804,9 @@ static __device__ __forceinline__ void ds_b8_hi(uint32_t a, uint32_t v) {
       (ds_b8_hi<snap_delta(k, D, 1)>(a, u[D]), ...);
     }
   }
-  template <int J, bool CHECKED, int WE>
+  template <int J, bool CHECKED, int WE, bool G, bool CHK>
   __device__ __forceinline__ void col(uint32_t (&M)[kDw], uint32_t (&Pq)[kPq], const uint32_t (&Pw)[kPw],
-                                      uint32_t tr0, uint32_t& s_next) {
+                                      uint32_t tr0, uint32_t& s_next, uint64_t dead, bool& ok) {
     if constexpr (WE > 0) walk_col<J, WE>();
     uint32_t P;
     if constexpr ((DBG & 8) != 0) {
@@ -777,7 +818,11 @@ static __device__ __forceinline__ void ds_b8_hi(uint32_t a, uint32_t v) {
     }
     constexpr int r = J % RT::steps;
     constexpr int c = J + 1;                           // column index within the body after the step
-    column5<J % 6, r, (J + 2) % 8>(M, P, K);
+    column5<J % 6, r, (J + 2) % 8, G>(M, P, K);
+    if constexpr (CHK && (c == 6 || c == 12 || c == 18)) {   // guard-free body: some state has H <= 115
+      const uint64_t pass = __builtin_amdgcn_ballot_w64((uint16_t)M[0] < (uint16_t)0x7400u) | dead;
+      ok = ok & rows_all_any(pass);                    // (no short-circuit: a branch would split the body)
+    }
     if constexpr (c % 8 == 6 && !(DBG & 2)) {
       snapshot<(c >> 3)>(M, std::make_integer_sequence<int, kDw>{});
       // A deferred walk (WE > 0) reads, in this body, slots that this body's snapshots then
@@ -803,15 +848,19 @@ static __device__ __forceinline__ void ds_b8_hi(uint32_t a, uint32_t v) {
   static __device__ __forceinline__ void pq_fill(uint32_t (&Pq)[kPq], const uint32_t (&Pw)[kPw], std::integer_sequence<int, Q...>) {
     ((Pq[Q] = bcast<Q>(Pw)), ...);
   }
-  template <bool CHECKED, int WE, int... J>
-  __device__ __forceinline__ void body(uint32_t (&M)[kDw], const uint32_t (&Pw)[kPw], uint32_t tr0, uint32_t& s_next,
-                                       std::integer_sequence<int, J...>) {
+  // G: guard ANDs in every column; CHK: the guard-free body's H_min checks (returns whether
+  // they all passed; rows in `dead` pass).  Rates 1/2 and 2/3 never need the guard.
+  template <bool CHECKED, int WE, bool G, bool CHK, int... J>
+  __device__ __forceinline__ bool body(uint32_t (&M)[kDw], const uint32_t (&Pw)[kPw], uint32_t tr0, uint32_t& s_next,
+                                       std::integer_sequence<int, J...>, uint64_t dead = 0) {
     uint32_t Pq[kPq];
+    bool ok = true;
     if constexpr (!(DBG & 8)) pq_fill(Pq, Pw, std::make_integer_sequence<int, kPq>{});
-    (col<J, CHECKED, WE>(M, Pq, Pw, tr0, s_next), ...);
+    (col<J, CHECKED, WE, G, CHK>(M, Pq, Pw, tr0, s_next, dead, ok), ...);
     // the tracebacks after a body read the slots its snapshots wrote (half 1 by asm stores
     // without a memory clobber): no load moves above this point
     asm volatile("" ::: "memory");
+    return ok;
   }
 };
 
@@ -886,6 +935,8 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
                          uint32_t rib, uint8_t* ring_block, uint8_t* __restrict__ out, uint32_t ooff,
                          uint32_t (&M)[kDw], RowX* rowx, uint2* __restrict__ dumps, bool prio, bool younger) {
   using RT = Rate<CR>;
+  // guard ANDs outside the speculative bodies: rate 3/4 only (Guard-free columns)
+  constexpr bool kG = CR == 2 || !kNoGuard;
   Walk W;
   W.we = 0;
   W.A = 0;
@@ -1043,7 +1094,19 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
       publish();
       pwords(Pw, base);
       pk.ring = ring_block + slot * kSlotBytes;
-      pk.template body<false, 0>(M, Pw, tr0, s_next, cols24);
+      if constexpr (CR == 2 && kNoGuard) {             // speculative guard-free body, redone on a failed check
+        uint32_t M0[kDw];
+#pragma unroll
+        for (int d = 0; d < kDw; d++) M0[d] = M[d];
+        const uint64_t dead = __builtin_amdgcn_ballot_w64(!R.live);
+        if (!pk.template body<false, 0, false, true>(M, Pw, tr0, s_next, cols24, dead)) {
+#pragma unroll
+          for (int d = 0; d < kDw; d++) M[d] = M0[d];
+          pk.template body<false, 0, true, false>(M, Pw, tr0, s_next, cols24);
+        }
+      } else {
+        pk.template body<false, 0, kG, false>(M, Pw, tr0, s_next, cols24);
+      }
       next_body();
       if constexpr ((DBG & 16) != 0) {                 // no events: stop at the input's end
         if (tr0 >= R.cols) R.live = false;
@@ -1058,7 +1121,7 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
       publish();
       pwords(Pw, base);
       pk.ring = ring_block + slot * kSlotBytes;
-      pk.template body<true, 0>(M, Pw, tr0, s_next, cols24);
+      pk.template body<true, 0, kG, false>(M, Pw, tr0, s_next, cols24);
     }
     if ((DBG & 1) == 0 && __builtin_amdgcn_ballot_w64(R.ppend) != 0) {
       traceback<true>(R.ppend, R.pM, R.pT, 256u, R.plook, l, rib, ring_block, out, ooff, R.nbytes, &W, tr0);
@@ -1077,8 +1140,8 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
       publish();
       pwords(Pw, base);
       pk.ring = ring_block + slot * kSlotBytes;
-      if (W.we == 3) pk.template body<true, 3>(M, Pw, tr0, s_next, cols24);
-      else pk.template body<true, 2>(M, Pw, tr0, s_next, cols24);
+      if (W.we == 3) pk.template body<true, 3, kG, false>(M, Pw, tr0, s_next, cols24);
+      else pk.template body<true, 2, kG, false>(M, Pw, tr0, s_next, cols24);
       W.we = 0;
       if ((DBG & 1) == 0 && __builtin_amdgcn_ballot_w64(R.fpend) != 0) {   // (a partial window is 256 columns on)
         traceback(R.fpend, R.fM, R.fT, R.fcnt, R.flook, l, rib, ring_block, out, ooff, R.nbytes);
