@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 4: speculative checked bodies -- parity, A/B against HEAD (prev)
+# the guarded build (libziria_rx.guard.so, -DZRX_NOGUARD=0) on configs 3, 2 and 5.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -2 gpurun_out/pytest_gpu.log
+VARIANTS="cur prev" ROUNDS=3 STEPS=20 AB_TAG=c3 bash scripts/gpu_ab_lib.sh || exit 1
+VARIANTS="cur prev" ROUNDS=2 STEPS=20 AB_TAG=c2 BENCH_ARGS="--config 2" bash scripts/gpu_ab_lib.sh || exit 1
+VARIANTS="cur prev" ROUNDS=2 STEPS=10 AB_TAG=c5 BENCH_ARGS="--config 5 --cpu-seconds 0.5" bash scripts/gpu_ab_lib.sh || exit 1
+echo r04e-ok

@@ -249,7 +249,9 @@ __device__ __forceinline__ void column5(uint32_t (&M)[kDw], uint32_t P, const Co
 // then for every column t + 1 of the body H_max(t) <= H_min(c) + 112 <= 227 with c the check
 // at or after t - 6 (columns 0..5 use the previous body, H_min <= 0 after its normalize), so
 // no add wrapped (induction over t) and the body is exact.  Otherwise the wave redoes the body
-// from its saved metrics with the guard (config 3 never does: its H stays below 84).  Each
+// from its saved metrics with the guard (config 3 never does: its H stays below 84).  Bodies
+// with events run speculatively as well: the row state (Row, its RowX entry, s_next) is saved
+// with the metrics, and a body with a deferred traceback walk is redone without the walk.  Each
 // check is one 16-bit compare of one half per lane (any state <= 115 suffices) and a ballot.
 #ifndef ZRX_NOGUARD
 #define ZRX_NOGUARD 1
@@ -1121,7 +1123,24 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
       publish();
       pwords(Pw, base);
       pk.ring = ring_block + slot * kSlotBytes;
-      pk.template body<true, 0, kG, false>(M, Pw, tr0, s_next, cols24);
+      if constexpr (CR == 2 && kNoGuard) {             // speculative too: events restored with the metrics
+        uint32_t M0[kDw];
+#pragma unroll
+        for (int d = 0; d < kDw; d++) M0[d] = M[d];
+        const Row R0 = R;
+        const RowX x0 = rowx[rib];
+        const uint32_t s0 = s_next;
+        if (!pk.template body<true, 0, false, true>(M, Pw, tr0, s_next, cols24, __builtin_amdgcn_ballot_w64(!R.live))) {
+#pragma unroll
+          for (int d = 0; d < kDw; d++) M[d] = M0[d];
+          R = R0;
+          rowx[rib] = x0;
+          s_next = s0;
+          pk.template body<true, 0, true, false>(M, Pw, tr0, s_next, cols24);
+        }
+      } else {
+        pk.template body<true, 0, kG, false>(M, Pw, tr0, s_next, cols24);
+      }
     }
     if ((DBG & 1) == 0 && __builtin_amdgcn_ballot_w64(R.ppend) != 0) {
       traceback<true>(R.ppend, R.pM, R.pT, 256u, R.plook, l, rib, ring_block, out, ooff, R.nbytes, &W, tr0);
@@ -1140,8 +1159,31 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
       publish();
       pwords(Pw, base);
       pk.ring = ring_block + slot * kSlotBytes;
-      if (W.we == 3) pk.template body<true, 3, kG, false>(M, Pw, tr0, s_next, cols24);
-      else pk.template body<true, 2, kG, false>(M, Pw, tr0, s_next, cols24);
+      if constexpr (CR == 2 && kNoGuard) {
+        // speculative: on a failed check the body is redone without the walk, whose reads all
+        // came before this body's snapshot stores and from verified bodies' slots (Walk), so
+        // its bytes already stored are right
+        uint32_t M0[kDw];
+#pragma unroll
+        for (int d = 0; d < kDw; d++) M0[d] = M[d];
+        const Row R0 = R;
+        const RowX x0 = rowx[rib];
+        const uint32_t s0 = s_next;
+        const uint64_t dead = __builtin_amdgcn_ballot_w64(!R.live);
+        const bool ok = W.we == 3 ? pk.template body<true, 3, false, true>(M, Pw, tr0, s_next, cols24, dead)
+                                  : pk.template body<true, 2, false, true>(M, Pw, tr0, s_next, cols24, dead);
+        if (!ok) {
+#pragma unroll
+          for (int d = 0; d < kDw; d++) M[d] = M0[d];
+          R = R0;
+          rowx[rib] = x0;
+          s_next = s0;
+          pk.template body<true, 0, true, false>(M, Pw, tr0, s_next, cols24);
+        }
+      } else {
+        if (W.we == 3) pk.template body<true, 3, kG, false>(M, Pw, tr0, s_next, cols24);
+        else pk.template body<true, 2, kG, false>(M, Pw, tr0, s_next, cols24);
+      }
       W.we = 0;
       if ((DBG & 1) == 0 && __builtin_amdgcn_ballot_w64(R.fpend) != 0) {   // (a partial window is 256 columns on)
         traceback(R.fpend, R.fM, R.fT, R.fcnt, R.flook, l, rib, ring_block, out, ooff, R.nbytes);
