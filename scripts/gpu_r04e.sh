@@ -1,6 +1,5 @@
 #!/bin/bash
-# Round 4: speculative checked bodies -- parity, A/B against HEAD (prev)
-# the guarded build (libziria_rx.guard.so, -DZRX_NOGUARD=0) on configs 3, 2 and 5.
+# Round 4: A/B of the working tree (cur) against HEAD (prev, scripts/build_variant.sh HEAD prev) after the GPU parity suite
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }

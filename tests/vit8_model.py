@@ -4,10 +4,15 @@ One packet = 8 lanes x 4 dwords x 2 16-bit halves = 64 trellis positions, so a w
 8 rows (k_viterbi3 with kLanes = 8).  Position bits 0..2 live inside the lane (half, dword
 bits 0 and 1), bits 3..5 are lane bits mapped to lane xor 1, 2, 7: DPP quad_perm, quad_perm
 and row_half_mirror inside each 8-lane group.  The column is vit3_model's shift-free step5
-(labels rotate: position p holds state rotl6(p, t mod 6); partner bit 5 - t mod 6), so the
-half format, markers, snapshot bytes and traceback are unchanged; what changes is which
-partner is a DPP move (phases 0..2), a dword swap (phases 3, 4: dword d ^ 2, d ^ 1) or the
-half swap (phase 5), and which dwords share a branch-metric word:
+(labels rotate: position p holds state rotl6(p, t mod 6); partner bit 5 - t mod 6), with the
+round-4 half format: [bit 15: 0][H >> 1 in bits 14..8][the cycle's decisions in bits 7..0, the
+column with cycle phase KPH writing its marker at bit KPH], branch metrics halved (BM / 2 =
+v ^ (e ? 7 : 0)) so P's bytes are 3-bit soft values, and no carry guard: a half's sum
+(H >> 1) + BM / 2 < 256 never leaves its 16 bits, and a wrap of the reference's u8 metric
+shows as bit 15, which the guarded column clears after each add (zrx_viterbi3.hpp "Guard-free
+columns").  A snapshot byte is bits 7..0 as they are.  What the 8-lane layout changes is
+which partner is a DPP move (phases 0..2), a dword swap (phases 3, 4: dword d ^ 2, d ^ 1) or
+the half swap (phase 5), and which dwords share a branch-metric word:
   a position bit flips state bit (b + ph) % 6, and flipping state bit 3 changes neither
   expected bit nor the marker, bit 5 only the marker, two bits that each flip A and B
   (bits 1, 2) nothing — see bx_source().
@@ -47,19 +52,14 @@ def expected(j):
     return ((j >> 1) ^ (j >> 2) ^ (j >> 4)) & 1, (j ^ (j >> 1) ^ (j >> 2)) & 1, (j >> 5) & 1
 
 
-def sel_word(ph, l, d, k7=False):
-    """v_perm selector of (phase, lane, dword): [BM_hi][bm_hi<<7][BM_lo][bm_lo<<7]
-    (k7: the snapshot-column form [BM + bm][0], byte 4 + 2A + B of {P | 0x01010101 : P})."""
+def sel_word(ph, l, d):
+    """v_perm selector of (phase, lane, dword): per half [P byte 2A + B][marker byte or 0]."""
     w = 0
     for h in range(2):
         j = V3.rotl6(int(POS[l, d, h]), ph)
         A, B, bm = expected(j)
-        if k7:
-            w |= 12 << (16 * h)
-            w |= (2 * A + B + (4 if bm else 0)) << (16 * h + 8)
-        else:
-            w |= (4 if bm else 12) << (16 * h)
-            w |= (2 * A + B) << (16 * h + 8)
+        w |= (4 if bm else 12) << (16 * h)
+        w |= (2 * A + B) << (16 * h + 8)
     return w
 
 
@@ -107,7 +107,7 @@ def partner(T, ph):
 class Packet(V3.Packet):
     def __init__(self, frame_len, code_rate):
         self.fl, self.cr = frame_len, code_rate
-        st = np.where(POS == 0, 0, 48).astype(np.uint32)
+        st = np.where(POS == 0, 0, 48 >> 1).astype(np.uint32)            # H >> 1 of ALL_INIT0
         self.M = ((st[..., 1] << 24) | (st[..., 0] << 8)).astype(np.uint32)   # [8, 4]
         self.ring = np.zeros((RING, 64), np.uint8)
         self.tr = 0
@@ -117,40 +117,36 @@ class Packet(V3.Packet):
         self.done = False
         self.v5 = True
         self.guard = True         # False: the guard-free column (zrx_viterbi3.hpp "Guard-free columns")
-        self.carries = 0          # low-half carries into bit 16 (guard-free: must stay 0)
+        self.carries = 0          # halves whose sum set bit 15 (a metric wrap; guard-free: must stay 0)
 
     def step5(self, kind, a, b):
         ph = self.tr % 6
         c = self.tr + 1
         k = (c + 1) % 8
-        if k == 0 or self.guard:
-            T = (self.M & (0xFE00FE00 if k == 0 else 0xFFFEFFFF)).astype(np.uint32)
-        else:
-            T = self.M.copy()
-        mk = 2 << k
-        P = V3.p_word(kind, a, b)
+        T = (self.M & 0x7F007F00).astype(np.uint32) if k == 0 else self.M.copy()
+        mk = 1 << k
+        P = (V3.p_word(kind, a, b) >> 1) & 0x7F7F7F7F           # BM / 2 per byte
         BX = np.zeros((NL, ND), np.uint32)
-        mbits = 0x01000100 if k == 7 else mk * 0x00010001
+        mbits = mk * 0x00010001
         for d in range(ND):
             src = bx_source(ph, d)
             if src[0] == "perm":
-                if k == 7:
-                    BX[:, d] = V3.perm(P | 0x01010101, P, [sel_word(ph, l, d, k7=True) for l in range(NL)])
-                else:
-                    BX[:, d] = V3.perm(mk * 0x01010101, P, SEL[ph, :, d])
+                BX[:, d] = V3.perm(mk * 0x01010101, P, SEL[ph, :, d])
             elif src[0] == "same":
                 BX[:, d] = BX[:, src[1]]
             else:
                 BX[:, d] = BX[:, src[1]] ^ mbits
-        K = 28 if kind == V3.FULL else 14
-        C = ((K + 1) << 8) * 0x00010001 if k == 7 else ((K << 8) | mk) * 0x00010001
+        K = 14 if kind == V3.FULL else 7
+        C = ((K << 8) | mk) * 0x00010001
         BY = ((C - BX.astype(np.int64)) & 0xFFFFFFFF).astype(np.uint32)
         add = lambda x, y: ((x.astype(np.uint64) + y) & 0xFFFFFFFF).astype(np.uint32)
-        lo_carry = lambda x, y: int((((x.astype(np.uint64) & 0xFFFF) + (y.astype(np.uint64) & 0xFFFF)) > 0xFFFF).sum())
+        wraps = lambda x: int(((x & 0x80008000) != 0).sum())
         Tp = partner(T, ph)
-        self.carries += lo_carry(T, BX) + (0 if Tp is None else lo_carry(Tp, BY))
         Z = V3.pk_add(V3.swap_halves(T), BY) if Tp is None else add(Tp, BY)
         X = add(T, BX)
+        self.carries += wraps(X) + wraps(Z)
+        if self.guard:                                        # the u8 wrap: bit 15 of a half
+            X, Z = X & 0x7FFF7FFF, Z & 0x7FFF7FFF
         self.M = V3.pk_min(X, Z)
         self.tr += 1
         if self.tr % 8 == 6:
@@ -159,7 +155,7 @@ class Packet(V3.Packet):
                 for d in range(ND):
                     for h in range(2):
                         s = V3.rotl6(int(POS[l, d, h]), self.tr)
-                        self.ring[slot, s] = (int(self.M[l, d]) >> (16 * h + 1)) & 0xFF
+                        self.ring[slot, s] = (int(self.M[l, d]) >> (16 * h)) & 0xFF
 
     def traceback(self, Mt, T, cnt, look):
         # the v3 traceback over this layout's positions
@@ -169,9 +165,9 @@ class Packet(V3.Packet):
                 for h in range(2):
                     half = (int(Mt[l, d]) >> (16 * h)) & 0xFFFF
                     s = V3.rotl6(int(POS[l, d, h]), T)
-                    m = ((half >> 8) & 0xFE) | ((half >> ((T + 1) % 8 + 1)) & 1)
+                    m = ((half >> 7) & 0xFE) | ((half >> ((T + 1) % 8)) & 1)
                     n = (T - 6) % 8
-                    pad = (((half >> 1) & ((1 << n) - 1)) << (8 - n)) & 0xFF
+                    pad = ((half & ((1 << n) - 1)) << (8 - n)) & 0xFF
                     key = ((m << 8) | (4 * s)) & 0xFFFF
                     key = key - 65536 if key >= 32768 else key
                     if best is None or key < best[0]:
@@ -210,7 +206,7 @@ def decode(soft, frame_len, code_rate, guard=True, stats=None):
         for k, kind in enumerate(kinds):
             P.step5(kind, *args[k])
             if stats is not None and P.tr % 24 in (6, 12, 18):
-                h = 2 * min(int(((P.M >> 9) & 0x7F).min()), int(((P.M >> 25) & 0x7F).min()))
+                h = 2 * min(int(((P.M >> 8) & 0x7F).min()), int(((P.M >> 24) & 0x7F).min()))
                 stats["max_check_hmin"] = max(stats.get("max_check_hmin", 0), h)
         if P.tr % 8 == 0:
             P.normalize()

@@ -14,15 +14,15 @@
 //    quad_perm, quad_perm, row_half_mirror), 16-lane rows bits 2..5 to lane xor 1, 2, 15, 8
 //    (quad_perm, quad_perm, row_mirror, row_ror:8), so each cross-lane partner is ONE DPP
 //    move inside the row.
-//  * Half = [H][pad]: H = the reference's u8 metric with its marker bit cleared (always
-//    even), the pad holds the decisions of the current 8-column cycle (column5).  The
-//    candidates of one column always differ in the marker, so v_pk_min_u16 reproduces
-//    min_epu8 on (metric | marker) exactly and drags the path history along with the
-//    winner (register exchange at no extra cost).  Every 8 columns the pads are stored to an
+//  * Half = [0][H >> 1][pad]: H = the reference's u8 metric with its marker bit cleared
+//    (always even) in bits 14..8, the pad (bits 7..0) holds the decisions of the current
+//    8-column cycle (column5).  The candidates of one column always differ in the marker,
+//    so v_pk_min_u16 reproduces min_epu8 on (metric | marker) exactly and drags the path
+//    history along with the winner (register exchange at no extra cost).  Every 8 columns the pads are stored to an
 //    LDS ring indexed by state: one byte there = 8 decoded bits, so the reference traceback
 //    (argmin of the signed (m<<8)|4s key, `lookahead` skipped columns, bytes from the end)
 //    becomes an argmin plus one dependent LDS read per output byte.
-//  * Branch metrics: a per-column pattern word P = [BM(A=0,B=0), BM(0,1), BM(1,0), BM(1,1)]
+//  * Branch metrics (halved, like H): P = [BM(A=0,B=0), BM(0,1), BM(1,0), BM(1,1)] / 2
 //    (implicit depuncturing: A-only / B-only columns have their own P, :93-110) is built
 //    once per 24-column body by the row's lanes and broadcast with ds_swizzle; a dword gets
 //    its branch metrics with one v_perm (per-lane selector) — or shares another dword's when
@@ -120,8 +120,7 @@ __device__ __forceinline__ uint32_t lds_addr(const uint8_t* p) {
 
 // Per-lane constants (registers for the whole kernel; entries no column reads are dropped).
 struct Consts {
-  uint32_t sel[6][kDw];   // v_perm selector: [BM_hi][bm_hi<<7][BM_lo][bm_lo<<7]
-  uint32_t sel7[3][kDw];  // KPH 7 columns (phases 1, 3, 5): [BM_hi + bm_hi][0][BM_lo + bm_lo][0]
+  uint32_t sel[6][kDw];   // v_perm selector: per half [P byte of the state's (A, B)][its marker byte or 0]
   uint32_t sa[3];         // LDS ring byte offset of the lane's first position (dword 0, half 0) at C mod 6 = 0,2,4
 };
 
@@ -130,7 +129,7 @@ __device__ __forceinline__ void make_consts(Consts& K, uint32_t l, uint32_t rib)
   for (int ph = 0; ph < 6; ph++) {
 #pragma unroll
     for (int d = 0; d < kDw; d++) {
-      uint32_t s = 0, s7 = 0;
+      uint32_t s = 0;
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         const uint32_t j = rotl6(pos_of(l, d, h), ph);
@@ -139,12 +138,8 @@ __device__ __forceinline__ void make_consts(Consts& K, uint32_t l, uint32_t rib)
         const uint32_t B = (j ^ (j >> 1) ^ (j >> 2)) & 1u;          // (encoding.blk:92-109)
         s |= (bm ? 4u : 12u) << (16 * h);
         s |= (2u * A + B) << (16 * h + 8);
-        // KPH 7: byte 2A+B of P (src1) or of P | 0x01010101 (src0: BM + 1, BM even), low byte 0
-        s7 |= 12u << (16 * h);
-        s7 |= (2u * A + B + (bm ? 4u : 0u)) << (16 * h + 8);
       }
       K.sel[ph][d] = s;
-      if (ph & 1) K.sel7[ph >> 1][d] = s7;
     }
   }
   // (the lane's other positions are at lane-uniform offsets from these: snap_delta)
@@ -161,28 +156,24 @@ __host__ __device__ constexpr uint32_t snap_delta(int k, int d, int h) {
   return o;
 }
 
-// Shift-free column (tests/vit3_model.py Packet.step5, vit8_model.py).  The column with
-// cycle phase KPH = (c + 1) mod 8 (c = the column computed; KPH 7 is the snapshot column)
-// writes its marker at bit KPH + 1 of each half: a half is [H >> 1 in bits 15..9][the cycle's
-// decisions in bits 8..1, oldest lowest][bit 0: carry guard].  Bits above the marker are
-// still 0 in both candidates (cleared at KPH 0), so the marker breaks ties exactly like the
-// brick's metric LSB (viterbicore.hpp:105-147), and the pads need no shift: one AND per
-// dword clears the guard bit 16 that a 32-bit add carries into when H0 wraps (at KPH 0 it
-// also clears the cycle's history).  At KPH 7 the marker is bit 8, the LSB of the (even) H
-// byte: BX = [BM][bm << 7] plus its own low byte = [BM + bm][0].
+// Shift-free column (tests/vit8_model.py).  The column with cycle phase KPH = (c + 1) mod 8
+// (c = the column computed; KPH 7 is the snapshot column) writes its marker at bit KPH of each
+// half: a half is [0][H >> 1 in bits 14..8][the cycle's decisions in bits 7..0, oldest
+// lowest].  Bits above the marker are still 0 in both candidates (cleared at KPH 0), so the
+// marker breaks ties exactly like the brick's metric LSB (viterbicore.hpp:105-147), and the
+// pads need no shift.  Branch metrics are added halved (BM / 2 at bit 8), so a half's sum
+// (H >> 1) + BM / 2 <= 127 + 14 stays inside its 16 bits and a 32-bit add serves two halves;
+// a wrap of the reference's u8 metric (H + BM > 255) sets bit 15, which the guarded column
+// (G) clears after each add ("Guard-free columns": it never happens in the others).  A
+// snapshot byte is bits 7..0 of a half as they are.
 template <int PH, int KPH, int D>
 __device__ __forceinline__ void column_bx(uint32_t (&BX)[kDw], uint32_t (&BY)[kDw], uint32_t P, const Consts& K,
                                           uint32_t C) {
-  constexpr uint32_t mk = 2u << KPH;
-  constexpr uint32_t mbits = KPH == 7 ? 0x01000100u : mk * 0x00010001u;
+  constexpr uint32_t mk = 1u << KPH;
+  constexpr uint32_t mbits = mk * 0x00010001u;
   constexpr int src = bx_src(PH, D);
   if constexpr (src < 0) {
-    if constexpr (KPH == 7) {      // [BM + bm][0] per half: BM (even) or BM + 1 = byte of P | 0x01010101
-      static_assert(PH & 1, "KPH 7 columns have odd phases (body columns 5, 13, 21)");
-      BX[D] = __builtin_amdgcn_perm(P | 0x01010101u, P, K.sel7[PH >> 1][D]);
-    } else {
-      BX[D] = __builtin_amdgcn_perm((mk & 0xFFu) * 0x01010101u, P, K.sel[PH][D]);
-    }
+    BX[D] = __builtin_amdgcn_perm(mk * 0x01010101u, P, K.sel[PH][D]);
   } else if constexpr ((src >> 8) == 0) {
     BX[D] = BX[src & 0xFF];
     BY[D] = BY[src & 0xFF];
@@ -195,11 +186,11 @@ __device__ __forceinline__ void column_bx(uint32_t (&BX)[kDw], uint32_t (&BY)[kD
   BY[D] = C - BX[D];
   asm("" : "+v"(BY[D]));
 }
-template <int PH, int D>
+template <int PH, bool G, int D>
 __device__ __forceinline__ void column_acs(uint32_t (&M)[kDw], const uint32_t (&T)[kDw], const uint32_t (&BX)[kDw],
                                            const uint32_t (&BY)[kDw]) {
   constexpr int pb = 5 - PH;                           // partner's position bit
-  const uint32_t X = T[D] + BX[D];
+  uint32_t X = T[D] + BX[D];
   uint32_t Z;
   if constexpr (pb == 0) {         // partner = the other half: [T.lo + BY.hi][T.hi + BY.lo] in one op
     asm("v_pk_add_u16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(Z) : "v"(T[D]), "v"(BY[D]));
@@ -208,20 +199,24 @@ __device__ __forceinline__ void column_acs(uint32_t (&M)[kDw], const uint32_t (&
   } else {                                             // partner lane: the DPP source of the add
     Z = (uint32_t)__builtin_amdgcn_mov_dpp((int)T[D], partner_dpp(pb), 0xF, 0xF, true) + BY[D];
   }
+  if constexpr (G) {                                   // the u8 wrap (bit 15 of a half)
+    X &= 0x7FFF7FFFu;
+    Z &= 0x7FFF7FFFu;
+  }
   M[D] = w32(__builtin_elementwise_min(h2(X), h2(Z)));
 }
-// G: clear the carry guard every column.  Without it (G false) the column is AND-free except
-// at KPH 0 (which clears the cycle's history anyway): see "Guard-free columns" below.
+// G: wrap the metrics mod 256 after every add (two ANDs per dword).  Without it (G false)
+// the column has no AND except at KPH 0, which clears the cycle's history: see "Guard-free
+// columns" below.
 template <int PH, int KIND, int KPH, bool G, int... D>
 __device__ __forceinline__ void column5_(uint32_t (&M)[kDw], uint32_t P, const Consts& K, std::integer_sequence<int, D...>) {
-  constexpr uint32_t mask = KPH == 0 ? 0xFE00FE00u : 0xFFFEFFFFu;
-  const uint32_t T[kDw] = {((KPH == 0 || G) ? (M[D] & mask) : M[D])...};
-  constexpr uint32_t mk = 2u << KPH;
-  constexpr uint32_t Kc = KIND == 0 ? 28u : 14u;
-  constexpr uint32_t C = KPH == 7 ? ((Kc + 1u) << 8) * 0x00010001u : ((Kc << 8) | mk) * 0x00010001u;
+  const uint32_t T[kDw] = {(KPH == 0 ? (M[D] & 0x7F007F00u) : M[D])...};
+  constexpr uint32_t mk = 1u << KPH;
+  constexpr uint32_t Kc = KIND == 0 ? 14u : 7u;        // (28 or 14) / 2: a column's complementary BM / 2
+  constexpr uint32_t C = ((Kc << 8) | mk) * 0x00010001u;
   uint32_t BX[kDw], BY[kDw];
   (column_bx<PH, KPH, D>(BX, BY, P, K, C), ...);
-  (column_acs<PH, D>(M, T, BX, BY), ...);
+  (column_acs<PH, G, D>(M, T, BX, BY), ...);
 }
 template <int PH, int KIND, int KPH, bool G = true>
 __device__ __forceinline__ void column5(uint32_t (&M)[kDw], uint32_t P, const Consts& K) {
@@ -229,10 +224,10 @@ __device__ __forceinline__ void column5(uint32_t (&M)[kDw], uint32_t P, const Co
 }
 
 // ---- Guard-free columns -------------------------------------------------------------------
-// The guard AND exists for one event: a low half whose H + BM passes 255 (the brick's u8
-// metric wraps) carries into bit 16.  Without wraps there are no carries, and the AND of the
-// columns with KPH 1..7 (84 of the hot body's 96 ANDs at rate 3/4) does nothing.  When can a
-// wrap happen?  H is exact integer arithmetic until the first wrap, bounded by:
+// The guard exists for one event: H + BM passing 255 (the brick's u8 metric wraps), which
+// sets bit 15 of a half; the guarded column clears it after each add (two ANDs per dword).
+// Without wraps there is nothing to clear.  When can a wrap happen?  H is exact integer
+// arithmetic until the first wrap, bounded by:
 //  * H_min never decreases from column to column (all branch metrics are >= 0) and grows by at
 //    most 14 per full column and 7 per punctured one (a state's two successors differ in both
 //    coded bits, so their branch metrics sum to 28 / 14);
@@ -248,7 +243,7 @@ __device__ __forceinline__ void column5(uint32_t (&M)[kDw], uint32_t P, const Co
 // columns 6, 12 and 18: if every check finds a state with H <= 115 (a row's H_min <= 115),
 // then for every column t + 1 of the body H_max(t) <= H_min(c) + 112 <= 227 with c the check
 // at or after t - 6 (columns 0..5 use the previous body, H_min <= 0 after its normalize), so
-// no add wrapped (induction over t) and the body is exact.  Otherwise the wave redoes the body
+// no add wrapped (induction over t) and the body is exact (half < 58 << 8: H >> 1 <= 57).  Otherwise the wave redoes the body
 // from its saved metrics with the guard (config 3 never does: its H stays below 84).  Bodies
 // with events run speculatively as well: the row state (Row, its RowX entry, s_next) is saved
 // with the metrics, and a body with a deferred traceback walk is redone without the walk.  Each
@@ -460,7 +455,7 @@ __device__ __forceinline__ void dump_load(const uint2* __restrict__ at, uint32_t
     M[2 * i] = v.x; M[2 * i + 1] = v.y;
   }
 }
-// do the H bits (& 0xFE00FE00) of two dumps differ in this lane?
+// do the H bits (& 0x7F007F00) of two dumps differ in this lane?
 __device__ __forceinline__ bool dump_ne(const uint2* __restrict__ a, const uint2* __restrict__ b, uint32_t l) {
   uint32_t x = 0;
 #pragma unroll
@@ -468,7 +463,7 @@ __device__ __forceinline__ bool dump_ne(const uint2* __restrict__ a, const uint2
     const uint2 u = a[(kDw / 2) * l + i], v = b[(kDw / 2) * l + i];
     x |= (u.x ^ v.x) | (u.y ^ v.y);
   }
-  return (x & 0xFE00FE00u) != 0u;
+  return (x & 0x7F007F00u) != 0u;
 }
 
 // Seam event of a row at relative column tr (a body end, after normalize): a segment stores
@@ -502,7 +497,7 @@ __device__ __forceinline__ void seam_event(Row& R, uint32_t tr, const uint32_t (
     uint32_t d = 0;
 #pragma unroll
     for (int i = 0; i < kDw; i++) d |= M[i] ^ B[i];
-    const uint64_t bad = __builtin_amdgcn_ballot_w64((d & 0xFE00FE00u) != 0u);
+    const uint64_t bad = __builtin_amdgcn_ballot_w64((d & 0x7F007F00u) != 0u);
     if (row_bits(bad) == 0u) {                         // the row's 64 H bytes agree
       R.cols = min(R.cols, seg_start(x.E, nseg, j) + kSegWarm + 30u - x.S);
       x.kn |= 1u << 17;
@@ -601,10 +596,11 @@ __device__ __forceinline__ void traceback(bool due, const uint32_t (&M)[kDw], ui
   for (int q = 0; q < 2 * kDw; q++) {
     const uint32_t half = M[q >> 1] >> (16 * (q & 1)) & 0xFFFFu;
     const uint32_t st = rotl6(pos_of(l, q >> 1, q & 1), ph);
-    // marker of column T at bit (T+1)%8 + 1; the n = (T-6)%8 newest decisions in bits n..1
+    // H in bits 14..8 (halved), the marker of column T at bit (T+1)%8; the n = (T-6)%8 newest
+    // decisions in bits n-1..0
     const uint32_t n = (T - 6u) & 7u;
-    const uint32_t m = ((half >> 8) & 0xFEu) | ((half >> (((T + 1u) & 7u) + 1u)) & 1u);
-    const uint32_t pad = (((half >> 1) & ((1u << n) - 1u)) << (8u - n)) & 0xFFu;   // as the shifted pad: newest at bit 7
+    const uint32_t m = ((half >> 7) & 0xFEu) | ((half >> ((T + 1u) & 7u)) & 1u);
+    const uint32_t pad = ((half & ((1u << n) - 1u)) << (8u - n)) & 0xFFu;   // as the shifted pad: newest at bit 7
     const uint32_t ukey = (((m << 8) | (st << 2)) & 0xFFFFu) ^ 0x8000u;   // signed int16 order
     best = min(best, (ukey << 16) | pad);
   }
@@ -703,27 +699,28 @@ __device__ __forceinline__ void traceback(bool due, const uint32_t (&M)[kDw], ui
 // [BM(0,0), BM(0,1), BM(1,0), BM(1,1)] = (2a replicated ^ X) + ((2b replicated & Mb) ^ Y),
 // with the lane's column kind in per-lane constants instead of selects (v_cndmask costs ~20
 // cycles per wave on gfx950, profiles/r01_ubench_isa_costs.log):
-//   full column (a on A, b on B): X = 0x0E0E0000, Mb = ~0, Y = 0x0E000E00
-//   A only:                        X = 0x0E0E0000, Mb = 0,  Y = 0
-//   B only (a on B):               X = 0x0E000E00, Mb = 0,  Y = 0
+// (halved: BM / 2 = e ? 7 - v : v = v ^ (e ? 7 : 0) for v = soft & 7)
+//   full column (a on A, b on B): X = 0x07070000, Mb = ~0, Y = 0x07000700
+//   A only:                        X = 0x07070000, Mb = 0,  Y = 0
+//   B only (a on B):               X = 0x07000700, Mb = 0,  Y = 0
 struct PKind {
   uint32_t X, Mb, Y;
 };
 __device__ __forceinline__ PKind p_kind(uint32_t r) {
-  return r == 0 ? PKind{0x0E0E0000u, 0xFFFFFFFFu, 0x0E000E00u}
-                : (r == 1 ? PKind{0x0E0E0000u, 0u, 0u} : PKind{0x0E000E00u, 0u, 0u});
+  return r == 0 ? PKind{0x07070000u, 0xFFFFFFFFu, 0x07000700u}
+                : (r == 1 ? PKind{0x07070000u, 0u, 0u} : PKind{0x07000700u, 0u, 0u});
 }
 // the same from bytes of an 8-byte pair {hi:lo}: selA / selB replicate byte a / b
 __device__ __forceinline__ uint32_t p_word_sel(const PKind& k, uint32_t hi, uint32_t lo, uint32_t selA, uint32_t selB) {
-  const uint32_t a2 = (__builtin_amdgcn_perm(hi, lo, selA) << 1) & 0x0E0E0E0Eu;
-  const uint32_t b2 = (__builtin_amdgcn_perm(hi, lo, selB) << 1) & (0x0E0E0E0Eu & k.Mb);
-  return (a2 ^ k.X) + (b2 ^ k.Y);
+  const uint32_t a1 = __builtin_amdgcn_perm(hi, lo, selA) & 0x07070707u;
+  const uint32_t b1 = __builtin_amdgcn_perm(hi, lo, selB) & (0x07070707u & k.Mb);
+  return (a1 ^ k.X) + (b1 ^ k.Y);
 }
 __device__ __forceinline__ uint32_t p_word(const PKind& k, uint32_t a, uint32_t b) {
-  // v replicated into 4 bytes (v_perm), doubled and masked to 2(v & 7) in each byte
-  const uint32_t a2 = (__builtin_amdgcn_perm(0u, a, 0u) << 1) & 0x0E0E0E0Eu;
-  const uint32_t b2 = (__builtin_amdgcn_perm(0u, b, 0u) << 1) & (0x0E0E0E0Eu & k.Mb);
-  return (a2 ^ k.X) + (b2 ^ k.Y);
+  // v replicated into 4 bytes (v_perm), masked to v & 7 in each byte
+  const uint32_t a1 = __builtin_amdgcn_perm(0u, a, 0u) & 0x07070707u;
+  const uint32_t b1 = __builtin_amdgcn_perm(0u, b, 0u) & (0x07070707u & k.Mb);
+  return (a1 ^ k.X) + (b1 ^ k.Y);
 }
 
 // DBG (timing experiments only, never selected by default): 1 skip the traceback walk,
@@ -786,7 +783,7 @@ static __device__ __forceinline__ void ds_b8_hi(uint32_t a, uint32_t v) {
   template <int k, int... D>
   __device__ __forceinline__ void snapshot(const uint32_t (&M)[kDw], std::integer_sequence<int, D...>) {
     uint8_t* s = ring + k * kSlotBytes;
-    const uint32_t u[kDw] = {(M[D] >> 1)...};
+    const uint32_t u[kDw] = {M[D]...};
     if constexpr (k == 2) {
       // C mod 6 = 4: position bits 0, 1 go to ring-index bits 1, 0, so (dword pair, half)
       // are 4 consecutive ring bytes, byte (h << 1) | (d & 1): one dword store per pair
@@ -822,7 +819,7 @@ static __device__ __forceinline__ void ds_b8_hi(uint32_t a, uint32_t v) {
     constexpr int c = J + 1;                           // column index within the body after the step
     column5<J % 6, r, (J + 2) % 8, G>(M, P, K);
     if constexpr (CHK && (c == 6 || c == 12 || c == 18)) {   // guard-free body: some state has H <= 115
-      const uint64_t pass = __builtin_amdgcn_ballot_w64((uint16_t)M[0] < (uint16_t)0x7400u) | dead;
+      const uint64_t pass = __builtin_amdgcn_ballot_w64((uint16_t)M[0] < (uint16_t)0x3A00u) | dead;
       ok = ok & rows_all_any(pass);                    // (no short-circuit: a branch would split the body)
     }
     if constexpr (c % 8 == 6 && !(DBG & 2)) {
@@ -1342,7 +1339,7 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
         } else {                                        // ALL_INIT0 (viterbilut.h:74-82)
 #pragma unroll
           for (int d = 0; d < v3::kDw; d++)
-            M[d] = ((v3::pos_of(l, d, 1) ? 48u : 0u) << 24) | ((v3::pos_of(l, d, 0) ? 48u : 0u) << 8);
+            M[d] = ((v3::pos_of(l, d, 1) ? 24u : 0u) << 24) | ((v3::pos_of(l, d, 0) ? 24u : 0u) << 8);   // 48 >> 1
         }
         // issue priority (run_rows): longest remaining first for a mixed batch's rows, the
         // younger wave's 2 of 3 bodies otherwise
