@@ -41,7 +41,6 @@ struct zrx_ctx {
 #ifdef ZRX_EXPERIMENTS
   // A/B builds only (scripts/build_variant.sh): environment knobs that select other kernels
   int v3dbg = 0;                  // ZRX_V3DBG: k_viterbi3 timing-experiment variants (wrong output)
-  int vit_impl = 3;               // ZRX_VITERBI 3: k_viterbi3; 2: k_viterbi2; 1: k_viterbi
 #endif
   hipStream_t stream = nullptr;
   bool timing = false;
@@ -307,9 +306,6 @@ static int ensure_eq_tables(zrx_ctx* c) {
 }
 
 static bool order_fits(const zrx_ctx* c, int npkts) {
-#ifdef ZRX_EXPERIMENTS
-  if (c->vit_impl != 3) return false;
-#endif
   return c->use_order && c->rows && npkts <= c->cap_pkts;
 }
 
@@ -354,14 +350,6 @@ static void launch_viterbi(zrx_ctx* c, const uint8_t* soft, const int64_t* soft_
   const int2* rows = plan ? c->rows : nullptr;
   int32_t* nrows = plan ? c->nrows : nullptr;
 #ifdef ZRX_EXPERIMENTS
-  if (c->vit_impl == 1) {
-    k_viterbi<<<blocks(npkts, 4), 256, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits, 256);
-    return;
-  }
-  if (c->vit_impl == 2) {
-    k_viterbi2<<<blocks(npkts, 4), 256, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits);
-    return;
-  }
   switch (c->v3dbg) {   // timing experiments (ZRX_V3DBG); 0 is the product kernel
 #define ZRX_V3(D) case D: k_viterbi3<D><<<g, b, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits, rows, nrows, nullptr, c->dumps); return;
     ZRX_V3(1) ZRX_V3(2) ZRX_V3(4) ZRX_V3(8) ZRX_V3(16) ZRX_V3(64) ZRX_V3(1024) ZRX_V3(1032)
@@ -427,18 +415,14 @@ int zrx_create(zrx_ctx** out, int device, void* stream) {
   ZRX_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_data_fft<true>, 256, 0));
   c->df_blocks_eq = std::max(1, occ) * c->ncu;
 #ifdef ZRX_EXPERIMENTS
-  if (const char* v = std::getenv("ZRX_VITERBI")) {
-    const int k = std::atoi(v);
-    c->vit_impl = (k >= 1 && k <= 3) ? k : 3;
-  }
   if (const char* v = std::getenv("ZRX_V3DBG")) c->v3dbg = std::atoi(v);
   if (const char* v = std::getenv("ZRX_ORDER")) c->use_order = std::atoi(v) != 0;
   if (const char* v = std::getenv("ZRX_CRCBLOCKS")) c->crc_blocks = std::atoi(v);
-  std::fprintf(stderr, "ziria_rx: EXPERIMENT build (vit_impl %d, v3dbg %d, order %d, crc_blocks %d)\n", c->vit_impl,
-               c->v3dbg, (int)c->use_order, c->crc_blocks);
+  std::fprintf(stderr, "ziria_rx: EXPERIMENT build (v3dbg %d, order %d, crc_blocks %d)\n", c->v3dbg, (int)c->use_order,
+               c->crc_blocks);
 #else
   static bool warned = false;
-  for (const char* k : {"ZRX_VITERBI", "ZRX_V3DBG", "ZRX_ORDER", "ZRX_CRCBLOCKS"})
+  for (const char* k : {"ZRX_V3DBG", "ZRX_ORDER", "ZRX_CRCBLOCKS"})
     if (std::getenv(k) && !warned) {
       std::fprintf(stderr, "ziria_rx: %s is an experiment-build knob (scripts/build_variant.sh); ignored by this "
                            "product build\n", k);

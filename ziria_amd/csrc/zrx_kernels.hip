@@ -10,16 +10,12 @@
 //                    + PilotTrack after the FFT (receiver.blk:66-71), also in k_signal_fft
 //   k_ofdm_eq        FFT -> ChannelEqualization -> PilotTrack, full 64-bin output
 //   k_viterbi3       (zrx_viterbi3.hpp) the batched brick driver loop, four packets per wave
-//   k_viterbi        (experiment builds only) one wave per packet, lane = trellis state
 //   k_descramble_crc one wave per packet: descrambler (Decode.blk:36-43) + CRC-32 check
 //                    (crc.blk:85-118), 64 lanes each on a chunk, CRC combined by GF(2) maps
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "zrx_device.hpp"
-#ifdef ZRX_EXPERIMENTS
-#include "zrx_viterbi2.hpp"   // k_viterbi2: A/B builds only (scripts/build_variant.sh)
-#endif
 #include "zrx_viterbi3.hpp"
 #include "zrx_frontend.hpp"
 #include "zrx_tx.hpp"
@@ -733,104 +729,6 @@ __global__ __launch_bounds__(256) void k_ofdm_eq(const uint4* __restrict__ sym, 
     for (int q = 0; q < 16; q++) dst[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
   }
 }
-
-#ifdef ZRX_EXPERIMENTS   // the v1 batched kernel (lane = state): A/B builds only
-// ------------------------------------------------------------------ Viterbi brick, batched (v1)
-// Decoder state of the brick driver loop (sora_ext_viterbi.cpp:66-153) for one packet.
-struct VitRun {
-  uint32_t m, tr, ob, total_bytes, tr_end, depth;
-  bool done;
-};
-
-// Post-group bookkeeping: normalize (:112-116) and the traceback schedule (:118-149).
-template <class Surv>
-__device__ __forceinline__ void vit_after_group(VitRun& v, int lane, Surv surv, uint8_t* __restrict__ out) {
-  if ((v.tr & 7u) == 0) v.m = vit_normalize(v.m);
-  uint32_t cnt = 0, look = 0;
-  if (v.tr >= v.tr_end) {
-    cnt = v.tr_end - v.ob - 6u;
-    look = v.tr - v.tr_end;
-    v.done = true;                                  // nothing can be output afterwards
-  } else if (v.tr >= v.ob + v.depth + 30u) {
-    cnt = v.depth;
-    look = 24u + (v.tr - (v.ob + v.depth + 30u)) % 8u;
-  }
-  if (cnt) {
-    vit_traceback(v.m, v.tr, cnt, look, lane, surv, out + v.total_bytes);
-    const uint32_t nb = cnt >> 3;
-    v.ob += cnt;
-    v.total_bytes += nb;
-  }
-}
-
-template <int USE>
-__device__ __forceinline__ void vit_step(VitRun& v, int a, int b, const VitLane& L, int lane, uint64_t* ring) {
-  v.m = acs<USE>(v.m, a, b, L);
-  v.tr++;
-  const uint64_t w = __ballot((v.m & 1u) != 0);
-  if (lane == 0) ring[v.tr & (kRing - 1)] = w;
-}
-
-// Runs all groups of one packet.  Soft values are read 192 at a time (48 dwords, one per
-// lane) and broadcast with readlane; 192 is a multiple of every group size (2, 3, 4).
-template <int CR>
-__device__ __forceinline__ void vit_packet(const uint8_t* __restrict__ sp, int n, VitRun& v, const VitLane& L,
-                                           int lane, uint64_t* ring, uint8_t* __restrict__ out) {
-  constexpr int G = CR == 0 ? 2 : (CR == 1 ? 3 : 4);
-  for (int base = 0; base < n && !v.done; base += 192) {
-    const uint32_t chunk = (lane < 48 && base + 4 * lane < n) ? *(const uint32_t*)(sp + base + 4 * lane) : 0u;
-    const int cn = min(192, n - base);
-    for (int k = 0; k < cn && !v.done; k += 12) {
-      const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)chunk, k >> 2);
-      const uint32_t d1 = (uint32_t)__builtin_amdgcn_readlane((int)chunk, (k >> 2) + 1);
-      const uint32_t d2 = (uint32_t)__builtin_amdgcn_readlane((int)chunk, (k >> 2) + 2);
-      int s[12];
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        s[q] = (d0 >> (8 * q)) & 0xFF; s[4 + q] = (d1 >> (8 * q)) & 0xFF; s[8 + q] = (d2 >> (8 * q)) & 0xFF;
-      }
-#pragma unroll
-      for (int g = 0; g < 12 / G; g++) {
-        if (v.done) break;
-        const int* q = s + g * G;
-        vit_step<3>(v, q[0], q[1], L, lane, ring);
-        if (CR == 2) { vit_step<1>(v, q[2], 0, L, lane, ring); vit_step<2>(v, q[3], 0, L, lane, ring); }
-        if (CR == 1) { vit_step<1>(v, q[2], 0, L, lane, ring); }
-        vit_after_group(v, lane, RingLds{ring}, out);
-      }
-    }
-  }
-}
-
-// vparams[4p..] = {frame_len, code_rate, soft_len, *}; out_bits[p] = bits written.
-__global__ __launch_bounds__(256) void k_viterbi(const uint8_t* __restrict__ soft, const int64_t* __restrict__ soft_off,
-                                                 const int32_t* __restrict__ vparams, int npkts,
-                                                 uint8_t* __restrict__ out, const int64_t* __restrict__ out_off,
-                                                 int32_t* __restrict__ out_bits, int depth) {
-  __shared__ uint64_t ring_all[4][kRing];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int p = blockIdx.x * 4 + wv;
-  if (p >= npkts) return;
-  uint64_t* ring = ring_all[wv];
-  const int32_t* vp = vparams + 4 * (int64_t)p;
-  const int fl = vp[0], cr = vp[1], n = vp[2];
-  VitRun v;
-  v.m = lane == 0 ? 0u : 48u;                       // ALL_INIT0 / ALL_INIT (viterbilut.h:74-82)
-  v.tr = 0; v.ob = 0; v.total_bytes = 0;
-  v.tr_end = (uint32_t)fl * 8u + 6u; v.depth = (uint32_t)depth; v.done = false;
-  if (lane == 0) ring[0] = 0;
-  const VitLane L = vit_lane(lane);
-  const uint8_t* sp = soft + soft_off[p];
-  uint8_t* op = out + out_off[p];
-  if (n > 0) {
-    if (cr == 0) vit_packet<0>(sp, n, v, L, lane, ring, op);
-    else if (cr == 1) vit_packet<1>(sp, n, v, L, lane, ring, op);
-    else if (cr == 2) vit_packet<2>(sp, n, v, L, lane, ring, op);
-  }
-  if (lane == 0) out_bits[p] = (int32_t)(v.total_bytes * 8u);
-}
-
-#endif  // ZRX_EXPERIMENTS
 
 // ------------------------------------------------------------------ descramble + CRC
 // info[8p+4] = crc_ok, info[8p+7] = viterbi bits; payload gets len-4 descrambled bytes.
