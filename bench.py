@@ -79,6 +79,8 @@ def main():
                          "turn, as a streaming receiver would, so one batch's tail overlaps the next one's head; "
                          "0 (default) = auto: 2 for an rx batch under %d packets per GPU (zrx_pipeline_link "
                          "mode 1) and for configs 2 and 5, else 1" % PIPELINE_BELOW)
+    ap.add_argument("--link", type=int, default=-1, choices=[-1, 0, 1, 2, 3],
+                    help="zrx_pipeline_link mode of two engines (-1: auto = 1 for configs 3/4, 0 for config 5)")
     ap.add_argument("--batches", type=int, default=2,
                     help="distinct input batches per GPU the steps rotate through (config 3/4/5)")
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 5])
@@ -127,8 +129,8 @@ def main():
     # is done, so only the short kernels around it overlap.
     engs = [RxEngine(local) for _ in range(npipe)]
     streams = [torch.cuda.Stream(dev) for _ in range(npipe)]
-    if npipe == 2:
-        engs[0].link(engs[1], 1)
+    if npipe == 2 and args.link != 0:
+        engs[0].link(engs[1], 1 if args.link < 0 else args.link)
     eng = engs[0]
     state = {}
 
@@ -413,6 +415,8 @@ def bench_mixed(args):
     # args.pipeline engines (own workspace and stream; auto: 2) take the steps in turn, as in main()
     engs = [RxEngine(0) for _ in range(args.pipeline or 2)]
     streams = [torch.cuda.Stream(dev) for _ in engs]
+    if len(engs) == 2 and args.link > 0:
+        engs[0].link(engs[1], args.link)
     outs = []
     for e in engs:
         e.reserve(n, S)

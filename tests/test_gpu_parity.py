@@ -372,3 +372,45 @@ def test_chain_split_plan_alternating_batches(engine):
     for i in np.nonzero(valid)[0][:512]:
         assert (pay[i, :m["meta"][i, 2] - 4] == m["payload"][i]).all(), i
     assert (runs["u"][0][1][:, 4] == 1).all()
+
+
+def test_chain_plan_reuse(engine):
+    """k_pkt_plan reuses the last plan when a batch is uniform and equal to the last planned
+    one in size and parameters (zrx_viterbi3.hpp PlanWord; k_signal_vit raises a mismatch
+    otherwise): uniform batches of one shape in turn (reused), the same size with other
+    parameters (rebuilt), the same size with one truncated packet (a mismatch raised by one
+    packet), a different size, and the first shape again; every batch's payloads equal what
+    was sent and the plan statistics match a fresh engine's."""
+    a = [txgen.make_batch(512, payload_len=1500, seed=90 + j, sigma=4.0, device="cuda") for j in range(2)]
+    b = txgen.make_batch(512, payload_len=700, seed=92, sigma=4.0, device="cuda")
+    c = txgen.make_batch(300, payload_len=1500, seed=93, sigma=4.0, device="cuda")
+    t = txgen.make_batch(512, payload_len=1500, seed=94, sigma=4.0, device="cuda")
+    nsym_t = t["nsym"].clone()
+    nsym_t[200] -= 5                                   # one truncated packet: status 2, no soft values
+    S = max(x["max_nsym"] for x in a + [b, c, t])
+    engine.reserve(512, S)
+    fresh = RxEngine(0)
+    fresh.reserve(512, S)
+
+    def check(x, nsym, pay, info, bad=()):
+        pay, info = pay.cpu().numpy(), info.cpu().numpy()
+        for i in range(nsym.numel()):
+            if i in bad:
+                assert info[i, 5] == 2 and info[i, 4] == 0, i
+            else:
+                assert info[i, 4] == 1 and (pay[i, :len(x["payload"][i])] == x["payload"][i]).all(), i
+
+    seq = [(a[0], a[0]["nsym"], ()), (a[1], a[1]["nsym"], ()), (a[0], a[0]["nsym"], ()), (b, b["nsym"], ()),
+           (a[1], a[1]["nsym"], ()), (t, nsym_t, (200,)), (a[1], a[1]["nsym"], ()), (c, c["nsym"], ()),
+           (a[0], a[0]["nsym"], ())]
+    for x, nsym, bad in seq:
+        pay, info = engine.rx(x["sym"], x["sym_off"], nsym, S)
+        st = engine.plan_stats()
+        pf, inf = fresh.rx(x["sym"], x["sym_off"], nsym, S)
+        torch.cuda.synchronize()
+        assert st == fresh.plan_stats()
+        fresh.close()
+        fresh = RxEngine(0)
+        fresh.reserve(512, S)
+        assert (pay == pf).all() and (info == inf).all()
+        check(x, nsym, pay, info, bad)

@@ -120,6 +120,24 @@ def crc_shift_tables(mats):
     return out
 
 
+def crc_shift_n_tables(mats, unit_bytes):
+    """Nibble-sliced register maps of n * unit_bytes zero bytes, n = 0..7 (n = 0: identity):
+    T[n][j][v] = image of (v << 4j) after those bytes (k_descramble_crc advances a lane's
+    register by 32 * (63 - lane) bytes as (63 - lane) & 7 chunks, then (63 - lane) >> 3 x 256)."""
+    apply = lambda M, v: __import__("functools").reduce(lambda a, i: a ^ (M[i] if (v >> i) & 1 else 0), range(32), 0)
+    out = []
+    for n in range(8):
+        nbytes = n * unit_bytes
+        ks = [k for k in range(len(mats)) if (nbytes >> k) & 1]
+        for j in range(8):
+            for v in range(16):
+                r = v << (4 * j)
+                for k in ks:
+                    r = apply(mats[k], r)
+                out.append(r)
+    return out
+
+
 def crc_slice4():
     """Slicing-by-4 tables: S[0] = the byte table, S[k][b] = S[k-1][b] after one zero byte."""
     T = crc_table()
@@ -184,6 +202,11 @@ def render():
     L.append("static constexpr uint8_t kScrB2[254] = {" + ", ".join(map(str, B2)) + "};")
     L.append("static constexpr uint32_t kScrW[127] = {" + ", ".join(f"0x{v:08x}u" for v in W) + "};")
     mats = crc_zero_mats(11)
+    for name, unit in (("kCrcShiftLo", 32), ("kCrcShiftHi", 256)):
+        Tn = crc_shift_n_tables(mats, unit)
+        L.append(f"// {name}[n][j*16+v]: CRC register image of (v << 4j) after n * {unit} zero bytes")
+        L.append(f"static constexpr uint32_t {name}[8][128] = {{" + ", ".join(
+            "{" + ", ".join(f"0x{x:08x}u" for x in Tn[128 * n:128 * n + 128]) + "}" for n in range(8)) + "};")
     T = crc_shift_tables(mats)
     L.append("// kCrcShift[k][j*16+v]: CRC register image of (v << 4j) after 32 * 2^k zero bytes")
     L.append("static constexpr uint32_t kCrcShift[6][128] = {" + ", ".join(

@@ -132,6 +132,10 @@ __global__ void k_fill_offsets(int64_t* off, int n, int64_t stride) {
 }
 
 static inline int blocks(int64_t n, int per) { return (int)((n + per - 1) / per); }
+#ifndef ZRX_SIGFFT_LANES
+#define ZRX_SIGFFT_LANES 64
+#endif
+constexpr int kSigFftLanes = ZRX_SIGFFT_LANES;
 
 // Trig tables of ChannelEqualization / PilotTrack: the reference LUTs (csrc/intalglutx.h:23,
 // :3667, :7351) in closed form, with pi written as 3.141593 as their generator did:
@@ -528,7 +532,8 @@ int zrx_reserve(zrx_ctx* c, int npkts, int max_nsym) {
   ZRX_CHECK(hipMalloc(&c->dec_bits, (size_t)np * 4 + 4));
   c->rows_cap = plan_rows_max(c, np);
   ZRX_CHECK(hipMalloc(&c->rows, (size_t)c->rows_cap * 8 + 8));
-  ZRX_CHECK(hipMalloc(&c->nrows, 32));
+  ZRX_CHECK(hipMalloc(&c->nrows, v3::kPlanWords * 4));
+  ZRX_CHECK(hipMemsetAsync(c->nrows, 0, v3::kPlanWords * 4, c->stream));   // (no plan to reuse)
   ZRX_CHECK(hipMalloc(&c->segs, (size_t)np + 16));
   ZRX_CHECK(hipMalloc(&c->order, (size_t)np * 4 + 16));
   ZRX_CHECK(hipMalloc(&c->dumps, (size_t)np * (v3::kMaxSeg - 1) * 2 * v3::kSeamWords * 8 + 256));
@@ -644,15 +649,19 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
     ev = c->evsets[c->nrec++].data();
   }
   if (ev) ZRX_CHECK(hipEventRecord(ev[0], s));
+  // one lane per packet, kSigFftLanes packets per one-wave block.  (16 measured worse: 9.4 ->
+  // 14.3 us at config 3, and with two engines in flight its 1024 single-wave blocks took CU
+  // slots the other batch's Viterbi blocks were placed by: config 5 101 -> 76 Gbit/s.)
   if (chan)
-    k_signal_fft<true><<<blocks(npkts, 64), 64, 0, s>>>((const uint4*)d_sym, d_sym_off, d_nsym, npkts,
-                                                          (uint4*)c->sig_soft, chan, T);
+    k_signal_fft<true><<<blocks(npkts, kSigFftLanes), kSigFftLanes, 0, s>>>((const uint4*)d_sym, d_sym_off, d_nsym,
+                                                                            npkts, (uint4*)c->sig_soft, chan, T);
   else
-    k_signal_fft<false><<<blocks(npkts, 64), 64, 0, s>>>((const uint4*)d_sym, d_sym_off, d_nsym, npkts,
-                                                           (uint4*)c->sig_soft, chan, T);
+    k_signal_fft<false><<<blocks(npkts, kSigFftLanes), kSigFftLanes, 0, s>>>((const uint4*)d_sym, d_sym_off, d_nsym,
+                                                                             npkts, (uint4*)c->sig_soft, chan, T);
   if (ev) ZRX_CHECK(hipEventRecord(ev[1], s));
-  k_signal_vit<<<blocks(npkts, 4), 256, 0, s>>>(c->sig_soft, d_nsym, npkts, c->cap_nsym, c->vparams, d_info);
   const bool ordered = order_fits(c, npkts);
+  k_signal_vit<<<blocks(npkts, 4), 256, 0, s>>>(c->sig_soft, d_nsym, npkts, c->cap_nsym, c->vparams, d_info,
+                                                 ordered ? c->nrows : nullptr);
   // A mixed batch's sort and row expansion (k_pkt_rows) only feed the Viterbi, so they can run
   // on a side stream while k_data_fft runs (config 5: -27 us a batch).  The fork and join cost
   // ~19 us of queue latency (config 3: +19 us) and a uniform batch has nothing to sort, so the

@@ -162,9 +162,11 @@ __device__ __forceinline__ int ndbps_of(int mod, int coding) {
 // info[8p..]    = {modulation, coding, len, header_err, crc_ok, status, symbols_used, viterbi_bits}
 // cap_nsym: symbols per packet the soft workspace holds (zrx_reserve); a packet whose header
 // asks for more gets ZRX_PKT_OVERSIZE and no soft values, so nothing writes past its slot.
+// plan (the rx chain's plan header, or null): a packet that asks for something else than the
+// uniform batch of npkts packets the last plan described raises kPlanMismatch (k_pkt_plan).
 __global__ __launch_bounds__(256) void k_signal_vit(const uint32_t* __restrict__ sig_soft, const int32_t* __restrict__ nsym,
                                                     int npkts, int cap_nsym, int32_t* __restrict__ vparams,
-                                                    int32_t* __restrict__ info) {
+                                                    int32_t* __restrict__ info, int32_t* plan) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int p = blockIdx.x * 4 + wv;
   if (p >= npkts) return;
@@ -202,6 +204,11 @@ __global__ __launch_bounds__(256) void k_signal_vit(const uint32_t* __restrict__
     int32_t* in = info + 8 * (int64_t)p;
     in[0] = mod; in[1] = cod; in[2] = len; in[3] = err; in[4] = 0; in[5] = status;
     in[6] = 1 + (status == 0 ? need : 0); in[7] = 0;
+    if (plan && plan[v3::kPlanExpN] == npkts &&
+        (plan[v3::kPlanExpLen] != vp[0] || plan[v3::kPlanExpCr] != vp[1] || plan[v3::kPlanExpSoft] != vp[2] ||
+         plan[v3::kPlanExpMod] != vp[3]) &&
+        *(volatile int32_t*)(plan + v3::kPlanMismatch) == 0)   // (once raised, no more atomics)
+      atomicOr(plan + v3::kPlanMismatch, 1);
   }
 }
 
@@ -401,8 +408,22 @@ __global__ __launch_bounds__(1024) void k_pkt_plan(const int32_t* __restrict__ v
   __shared__ uint2 round_total;
   __shared__ uint32_t hist[kOrderPerThread * 1024];
   __shared__ unsigned long long tcols;
-  __shared__ uint32_t rtotal, uniform;
+  __shared__ uint32_t rtotal, uniform, reuse;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  // The rx chain's batch equals the uniform batch the last plan described (k_signal_vit raised
+  // no mismatch): offsets, wave starts and the row header are all still right.  Otherwise the
+  // plan is rebuilt and forgets the old batch first.
+  if (t == 0) {
+    reuse = off && rows && nrows[v3::kPlanExpN] == npkts && nrows[v3::kPlanMismatch] == 0;
+    if (reuse) {
+      nrows[v3::kPlanFixes] = 0;                       // (counted afresh by this launch's seam pass)
+    } else {
+      nrows[v3::kPlanExpN] = 0;
+      nrows[v3::kPlanMismatch] = 0;
+    }
+  }
+  __syncthreads();
+  if (reuse) return;
   if (rows) {
     for (int i = t; i < kOrderPerThread * 1024; i += 1024) hist[i] = 0;
     if (t == 0) { tcols = 0; rtotal = 0; uniform = 1; }
@@ -426,7 +447,7 @@ __global__ __launch_bounds__(1024) void k_pkt_plan(const int32_t* __restrict__ v
         vu[i] = (n + 255u) >> 8;
         vs[i] = q.w == 3 ? n / 288u : (n >> (q.w & 3)) / 48u;   // soft_len / N_CBPS, constant divisors
         my_cols += cols_of(q.y, q.z);
-        same = same && q.x == q0.x && q.y == q0.y && q.z == q0.z;
+        same = same && q.x == q0.x && q.y == q0.y && q.z == q0.z && q.w == q0.w;
       }
     }
     if (!off) continue;
@@ -489,6 +510,11 @@ __global__ __launch_bounds__(1024) void k_pkt_plan(const int32_t* __restrict__ v
       nrows[v3::kPlanUniform] = (int32_t)n0;
       nrows[v3::kPlanDropped] = (uint32_t)npkts * n0 > (uint32_t)rows_cap ? (int32_t)((uint32_t)npkts * n0 - rows_cap) : 0;
       nrows[v3::kPlanNcu] = ncu;
+      if (off) {                                       // the batch a next launch may reuse this plan for
+        nrows[v3::kPlanExpLen] = q0.x; nrows[v3::kPlanExpCr] = q0.y;
+        nrows[v3::kPlanExpSoft] = q0.z; nrows[v3::kPlanExpMod] = q0.w;
+        nrows[v3::kPlanExpN] = npkts;
+      }
     }
     return;
   }
@@ -740,19 +766,21 @@ __global__ __launch_bounds__(256) void k_ofdm_eq(const uint4* __restrict__ sym, 
 //    first 4 bytes complemented equals the reference's all-ones-initialised one; leading
 //    zero bytes leave a zero register unchanged, so the payload is right-aligned in a
 //    2048-byte frame and lane L takes bytes [32L, 32L+32) as 8 dwords (slicing-by-4).  Each
-//    lane's register is advanced past the 32*(63-L) bytes behind its chunk with
-//    nibble-sliced zero-byte tables and the wave XORs the 64 registers.
+//    lane's register is advanced past the 32*(63-L) bytes behind its chunk with two
+//    nibble-sliced zero-byte tables of its own (((63-L) & 7) x 32 and ((63-L) >> 3) x 256
+//    bytes: 16 lookups, not one table per bit of 63-L) and the wave XORs the 64 registers.
 constexpr int kCrcWaves = 8;
 __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t* __restrict__ dec,
                                                                    const int32_t* __restrict__ dec_bits,
                                                                    int32_t* __restrict__ info, uint8_t* __restrict__ payload,
                                                                    int npkts) {
   __shared__ uint32_t s4[4][256];
-  __shared__ uint32_t shf[6][128];
+  __shared__ uint32_t shf[16][128];                   // [n]: n * 32 zero bytes, [8 + n]: n * 256
   __shared__ uint32_t scrw[128];
   __shared__ uint8_t scrb[256];
   for (int i = threadIdx.x; i < 1024; i += blockDim.x) s4[i >> 8][i & 255] = kCrcS4[i >> 8][i & 255];
-  for (int i = threadIdx.x; i < 768; i += blockDim.x) shf[i >> 7][i & 127] = kCrcShift[i >> 7][i & 127];
+  for (int i = threadIdx.x; i < 1024; i += blockDim.x) shf[i >> 7][i & 127] = kCrcShiftLo[i >> 7][i & 127];
+  for (int i = threadIdx.x; i < 1024; i += blockDim.x) shf[8 + (i >> 7)][i & 127] = kCrcShiftHi[i >> 7][i & 127];
   for (int i = threadIdx.x; i < 254; i += blockDim.x) scrb[i] = kScrB2[i];
   for (int i = threadIdx.x; i < 127; i += blockDim.x) scrw[i] = kScrW[i];
   __syncthreads();
@@ -833,13 +861,16 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
           r ^= x[j];
           r = s4[3][r & 0xFFu] ^ s4[2][(r >> 8) & 0xFFu] ^ s4[1][(r >> 16) & 0xFFu] ^ s4[0][r >> 24];
         }
-        const uint32_t adv = 63u - (uint32_t)lane;     // 32-byte chunks behind this one
+        // advance past the 63 - lane 32-byte chunks behind this one: (63 - lane) & 7 chunks,
+        // then (63 - lane) >> 3 times 256 bytes (the lane's two tables; entry 0 is the identity)
+        const uint32_t adv = 63u - (uint32_t)lane;
   #pragma unroll
-        for (int k = 0; k < 6; k++) {
+        for (int k = 0; k < 2; k++) {
+          const uint32_t* tb = shf[k ? 8u + (adv >> 3) : (adv & 7u)];
           uint32_t t = 0;
   #pragma unroll
-          for (int j = 0; j < 8; j++) t ^= shf[k][j * 16 + ((r >> (4 * j)) & 15u)];
-          if ((adv >> k) & 1u) r = t;
+          for (int j = 0; j < 8; j++) t ^= tb[j * 16 + ((r >> (4 * j)) & 15u)];
+          r = t;
         }
       }
       crc = ~wave_xor_u32(r);

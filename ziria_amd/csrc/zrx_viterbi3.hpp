@@ -389,7 +389,13 @@ __host__ __device__ __forceinline__ uint32_t rank_place(uint32_t r, uint32_t nfu
   return order_place(r * (uint32_t)kRows, nfull, ncu, rcp) / (uint32_t)kRows;
 }
 // The plan header k_pkt_plan writes for k_viterbi3 (int32 words of the nrows buffer).
-enum PlanWord { kPlanRows = 0, kPlanFixes = 1, kPlanUniform = 2, kPlanNcu = 3, kPlanSegLen = 4, kPlanDropped = 5 };   // (8 words)
+// Words 8..13: the uniform batch the arrays of the last rx-chain plan describe (kPlanExpN
+// packets, 0 = none, of these {frame_len, code_rate, soft_len, modulation}) and the flag
+// k_signal_vit raises when a packet of a batch of that size asks for something else: a
+// batch equal in all of it reuses the plan (k_pkt_plan returns at once).
+enum PlanWord { kPlanRows = 0, kPlanFixes = 1, kPlanUniform = 2, kPlanNcu = 3, kPlanSegLen = 4, kPlanDropped = 5,
+                kPlanExpN = 8, kPlanExpLen = 9, kPlanExpCr = 10, kPlanExpSoft = 11, kPlanExpMod = 12,
+                kPlanMismatch = 13, kPlanWords = 16 };
 
 // start unit m_k of segment k >= 1 of nseg over a frame of E = 8 len + 6 columns (rounded
 // k E / nseg; with E / nseg >= kMinCut the m_k are distinct (steps of > 1 unit) and
@@ -513,6 +519,7 @@ __device__ __forceinline__ void seam_event(Row& R, uint32_t tr, const uint32_t (
 }
 
 // Events after a group ending at column tr (sora_ext_viterbi.cpp:112-149); normalize ran first.
+// (Reads no LDS ring slot: see the snapshot-store invariant at Packet::ds_b8_hi.)
 __device__ __forceinline__ void events(Row& R, uint32_t tr, const uint32_t (&M)[kDw]) {
   if (R.live && tr >= R.next) {
     if (tr >= R.end) {                                  // final traceback
@@ -774,9 +781,21 @@ struct Packet {
       walk_stepk(*W, (uint32_t)(J + 12), (uint32_t)NL, ring0, rib * 64u);
     }
   }
+  // The half-1 snapshot bytes go out by asm without a memory clobber (one clobber per store
+  // cost 0.7-1.5 %), so the compiler does not see them as LDS writes.  Invariant: no LDS read
+  // of the ring may sit between a snapshot and the next compiler barrier — today the body's
+  // end (`body`) and, in bodies with a deferred walk, the barrier after each snapshot (`col`).
+  // events() and seam_event() read no ring slot (only rowx and global dumps); anything added
+  // to a checked body that does must add a barrier.  -DZRX_SNAP_CLOBBER builds the stores with
+  // the clobber: a parity A/B (scripts/build_flags_variant.sh) that shows a reordering as a
+  // mismatch.
   template <uint32_t O>
 static __device__ __forceinline__ void ds_b8_hi(uint32_t a, uint32_t v) {
+#ifdef ZRX_SNAP_CLOBBER
+  asm volatile("ds_write_b8_d16_hi %0, %1 offset:%2" ::"v"(a), "v"(v), "i"(O) : "memory");
+#else
   asm volatile("ds_write_b8_d16_hi %0, %1 offset:%2" ::"v"(a), "v"(v), "i"(O));
+#endif
 }
 // Snapshot k (column C = 8k + 6 of the body, C mod 6 = 2k): every position's pad byte
   // (bits 8..1 of its half) to the ring at the lane's first offset plus a lane-uniform delta.
