@@ -316,7 +316,9 @@ __device__ __forceinline__ void plan_rows_mixed(const int32_t* __restrict__ vpar
   // the second writes the rows there.  (Sorted by rate first, the blocks' lengths rise and
   // fall three times, and the snake over that order paired long blocks with long ones: config
   // 5's per-SIMD columns spread 768..11 614 around a mean of 9026.)
-  const uint32_t total = *rtotal, nfull = total / (uint32_t)v3::kRows;
+  // (ranked units: kPlanUnit rows — a wave's 8 for the dynamic queue of kDynMixed, else a
+  // block's 32 placed over the CUs)
+  const uint32_t total = *rtotal, nfull = total / (uint32_t)v3::kPlanUnit;
   const uint32_t ncu2 = (uint32_t)max(ncu, 2), ncu_rcp = 0xFFFFFFFFu / ncu2 + 1u;
   const bool ranked = ZRX_RANK_BLOCKS && nfull <= (uint32_t)v3::kRankBlocks;
   __shared__ uint32_t esum[16];
@@ -348,14 +350,14 @@ __device__ __forceinline__ void plan_rows_mixed(const int32_t* __restrict__ vpar
             const int4 q = *reinterpret_cast<const int4*>(vparams + 4 * (int64_t)pk[i]);
             const uint32_t cols = cols_of(q.y, q.z);
             const uint32_t len = ns[i] <= 1u ? cols : v3::udiv_small(min(cols, (1u << 20) - 1u) + ns[i] - 1u, ns[i]) + 286u;
-            for (uint32_t b = ex / (uint32_t)v3::kRows; b * (uint32_t)v3::kRows < ex + ns[i] && b < nfull; b++)
+            for (uint32_t b = ex / (uint32_t)v3::kPlanUnit; b * (uint32_t)v3::kPlanUnit < ex + ns[i] && b < nfull; b++)
               atomicMax(&blk[b], len);
           }
         } else {
           for (uint32_t k = 0; k < ns[i]; k++) {
-            const uint32_t pos = ex + k, b = pos / (uint32_t)v3::kRows;
-            const uint32_t at = !ranked ? v3::order_place(pos, nfull, ncu2, ncu_rcp)
-                                : b < nfull ? blk[b] * (uint32_t)v3::kRows + pos % (uint32_t)v3::kRows : pos;
+            const uint32_t pos = ex + k, b = pos / (uint32_t)v3::kPlanUnit;
+            const uint32_t at = !ranked ? (v3::kDynMixed ? pos : v3::order_place(pos, nfull, ncu2, ncu_rcp))
+                                : b < nfull ? blk[b] * (uint32_t)v3::kPlanUnit + pos % (uint32_t)v3::kPlanUnit : pos;
             if (at < (uint32_t)rows_cap) rows[at] = make_int2(pk[i], (int)(k | (ns[i] << 8)));   // (always: the plan's row bound)
           }
         }
@@ -382,7 +384,7 @@ __device__ __forceinline__ void plan_rows_mixed(const int32_t* __restrict__ vpar
         const uint32_t key = b < nfull ? (uint32_t)kOrderLen - 1u - min((blk[b] + 23u) / 24u, (uint32_t)kOrderLen - 1u) : 0u;
         const uint32_t r = order_claim(hist, b < nfull, key);
         __syncthreads();                               // every lane read blk[] before it is rewritten
-        if (b < nfull) blk[b] = v3::rank_place(r, nfull, ncu2, ncu_rcp);
+        if (b < nfull) blk[b] = v3::kDynMixed ? r : v3::rank_place(r, nfull, ncu2, ncu_rcp);   // (queue: rank order)
       }
       __syncthreads();
     }
@@ -395,6 +397,7 @@ __device__ __forceinline__ void plan_rows_mixed(const int32_t* __restrict__ vpar
     // bound must show (zrx_plan_check) instead of leaving packets silently undecoded
     nrows[v3::kPlanDropped] = total > (uint32_t)rows_cap ? (int32_t)(total - (uint32_t)rows_cap) : 0;
     nrows[v3::kPlanNcu] = (int32_t)ncu2;
+    nrows[v3::kPlanQueue] = 0;                         // (kDynMixed: the tasks' queue word)
   }
 }
 
@@ -784,9 +787,12 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
   for (int i = threadIdx.x; i < 254; i += blockDim.x) scrb[i] = kScrB2[i];
   for (int i = threadIdx.x; i < 127; i += blockDim.x) scrw[i] = kScrW[i];
   __syncthreads();
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // (packet values below: scalar)
   // grid-stride over packets (one wave per packet at a time): the LDS tables above are
-  // staged once per block, not once per 8 packets
+  // staged once per block, not once per 8 packets.  Decoded bytes are read and payload
+  // dwords written by buffer ops on the packet's own slot: 32-bit lane offsets, and a word
+  // outside the slot (load: 0) or past the payload (store: dropped) needs no branch.
   for (int p = blockIdx.x * kCrcWaves + wv; p < npkts; p += gridDim.x * kCrcWaves) {
     int32_t* in = info + 8 * (int64_t)p;
     const int len = in[2], status = in[5];
@@ -797,81 +803,76 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
       continue;
     }
     const uint8_t* d = dec + (int64_t)p * kDecStride;
-    const uint32_t* d32 = (const uint32_t*)d;
-    uint32_t* py32 = (uint32_t*)(payload + (int64_t)p * kPayloadStride);
+    const int plen = len - 4;
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)d, (short)0, kDecStride, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)(payload + (int64_t)p * kPayloadStride),
+                                                                         (short)0, (plen + 3) & ~3, 0x00020000);
     const uint32_t S = (uint32_t)d[1] >> 1;           // SERVICE bits 9..15 = scrambler state
     const uint32_t ksm = S == 0 ? 0u : 0xFFFFFFFFu;   // state 0 never leaves 0: zero keystream
     const int n0 = (16 * (int)kScrPhase[S]) % 127;
-    const int plen = len - 4;
     // payload: dword i = decoded bytes 2+4i .. 5+4i.  The lane's dwords i = lane + 64k
     // (k < 8: plen <= 2044) are all loaded before any is used (one memory latency per packet,
     // not one per iteration); the upper neighbour word comes from lane + 1.
-    uint32_t wv[9];
+    uint32_t wv9[9];
 #pragma unroll
-    for (int k = 0; k < 9; k++) {
-      const int i = lane + 64 * k;
-      wv[k] = 4 * i < plen + 4 ? d32[i] : 0u;          // words 0 .. (plen+3)/4 <= 512 of the slot
-    }
+    for (int k = 0; k < 9; k++) wv9[k] = __builtin_amdgcn_raw_buffer_load_b32(rd, 4 * (lane + 64 * k), 0, 0);
     int n = (n0 + 4 * lane) % 127;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       const int i = lane + 64 * k;
-      const uint32_t up = (uint32_t)__shfl_down((int)wv[k], 1);
-      const uint32_t nx = lane == 63 ? (uint32_t)__builtin_amdgcn_readlane((int)wv[k + 1], 0) : up;
-      if (4 * i < plen) {
-        uint32_t v = __builtin_amdgcn_alignbyte(nx, wv[k], 2) ^ (scrw[n] & ksm);
-        const int rem = plen - 4 * i;
-        if (rem < 4) v &= (1u << (8 * rem)) - 1u;
-        py32[i] = v;
-      }
+      const uint32_t dn = (uint32_t)__shfl_down((int)wv9[k], 1);
+      const uint32_t nx = lane == 63 ? (uint32_t)__builtin_amdgcn_readlane((int)wv9[k + 1], 0) : dn;
+      uint32_t v = __builtin_amdgcn_alignbyte(nx, wv9[k], 2) ^ (scrw[n] & ksm);
+      const int rem = plen - 4 * i;                    // (a dword at or past the payload end: dropped)
+      if (rem < 4) v &= rem > 0 ? 0xFFFFFFFFu >> (32 - 8 * rem) : 0u;
+      __builtin_amdgcn_raw_buffer_store_b32(v, rp, 4 * i, 0, 0);
       n += 2;                                          // 256 bytes on: 256 = 2 mod 127
       if (n >= 127) n -= 127;
     }
     uint32_t crc;
     if (plen >= 4) {
       const int q0 = 32 * lane - (2048 - plen);        // payload index of this lane's first byte
+      // (a chunk wholly before the payload: every word masked to 0 below, so r stays 0)
+      const int g = 2 + q0;                            // decoded-byte index of the first byte
+      const int a = g >> 2;                            // (arithmetic: negative before the slot)
+      const int sh = g & 3;
+      uint32_t w[9];
+#pragma unroll
+      for (int j = 0; j < 9; j++) w[j] = __builtin_amdgcn_raw_buffer_load_b32(rd, 4 * max(a + j, 0), 0, 0);
+      int m = (n0 + q0 + 127 * 17) % 127;              // (q0 > -2048 = -127 x 17 + 111)
+      uint32_t x[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        x[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh) ^ (scrw[m] & ksm);
+        m += 4;
+        if (m >= 127) m -= 127;
+      }
+      if (q0 < 4) {                                    // chunk holds the payload start (or lies before it)
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          const int qf = q0 + 4 * j;                   // payload index of byte 0 of word j
+          if (qf <= -4) x[j] = 0;
+          else if (qf < 0) x[j] &= 0xFFFFFFFFu << (-8 * qf);   // bytes before the payload
+          if (qf > -4 && qf < 4)                                // complement payload bytes 0..3
+            x[j] ^= qf >= 0 ? 0xFFFFFFFFu >> (8 * qf) : 0xFFFFFFFFu << (-8 * qf);
+        }
+      }
       uint32_t r = 0;
-      if (q0 + 32 > 0) {
-        const int g = 2 + q0;                          // decoded-byte index of the first byte
-        const int a = g >> 2;
-        const int sh = g & 3;
-        uint32_t w[9];
-  #pragma unroll
-        for (int j = 0; j < 9; j++) w[j] = d32[max(a + j, 0)];
-        int m = ((n0 + q0) % 127 + 127) % 127;
-        uint32_t x[8];
-  #pragma unroll
-        for (int j = 0; j < 8; j++) {
-          x[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh) ^ (scrw[m] & ksm);
-          m += 4;
-          if (m >= 127) m -= 127;
-        }
-        if (q0 < 4) {                                  // chunk holds the payload start
-  #pragma unroll
-          for (int j = 0; j < 8; j++) {
-            const int qf = q0 + 4 * j;                 // payload index of byte 0 of word j
-            if (qf <= -4) x[j] = 0;
-            else if (qf < 0) x[j] &= 0xFFFFFFFFu << (-8 * qf);   // bytes before the payload
-            if (qf > -4 && qf < 4)                                // complement payload bytes 0..3
-              x[j] ^= qf >= 0 ? 0xFFFFFFFFu >> (8 * qf) : 0xFFFFFFFFu << (-8 * qf);
-          }
-        }
-  #pragma unroll
-        for (int j = 0; j < 8; j++) {
-          r ^= x[j];
-          r = s4[3][r & 0xFFu] ^ s4[2][(r >> 8) & 0xFFu] ^ s4[1][(r >> 16) & 0xFFu] ^ s4[0][r >> 24];
-        }
-        // advance past the 63 - lane 32-byte chunks behind this one: (63 - lane) & 7 chunks,
-        // then (63 - lane) >> 3 times 256 bytes (the lane's two tables; entry 0 is the identity)
-        const uint32_t adv = 63u - (uint32_t)lane;
-  #pragma unroll
-        for (int k = 0; k < 2; k++) {
-          const uint32_t* tb = shf[k ? 8u + (adv >> 3) : (adv & 7u)];
-          uint32_t t = 0;
-  #pragma unroll
-          for (int j = 0; j < 8; j++) t ^= tb[j * 16 + ((r >> (4 * j)) & 15u)];
-          r = t;
-        }
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        r ^= x[j];
+        r = s4[3][r & 0xFFu] ^ s4[2][(r >> 8) & 0xFFu] ^ s4[1][(r >> 16) & 0xFFu] ^ s4[0][r >> 24];
+      }
+      // advance past the 63 - lane 32-byte chunks behind this one: (63 - lane) & 7 chunks,
+      // then (63 - lane) >> 3 times 256 bytes (the lane's two tables; entry 0 is the identity)
+      const uint32_t adv = 63u - (uint32_t)lane;
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        const uint32_t* tb = shf[k ? 8u + (adv >> 3) : (adv & 7u)];
+        uint32_t t = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) t ^= tb[j * 16 + ((r >> (4 * j)) & 15u)];
+        r = t;
       }
       crc = ~wave_xor_u32(r);
     } else {                                           // < 4 payload bytes: the plain register
