@@ -92,3 +92,20 @@ def test_guard_free_columns(golden, oracle, cr):
         assert st["carries"] == 0 and (got == oracle.viterbi_decode(s, 300, cr)).all()
         if cr == 2 and noise >= 0:
             assert st["max_check_hmin"] <= 115
+
+
+def test_signal_rows_model(golden, oracle):
+    """The SIGNAL decode on 8-lane rows (k_signal_vit) against the reference's SIGNAL vectors
+    and the oracle's Viterbi_sig11 on random and near-clean soft values."""
+    g = golden["ref_viterbi"]
+    for s, exp in list(zip(g["sig_soft"], g["sig_bits"]))[::4]:
+        hb = V.signal_header_bits(s)
+        assert hb.to_bytes(3, "little") == bytes(exp)
+    rng = np.random.default_rng(21)
+    for i in range(120):
+        if i % 2:
+            s = rng.integers(0, 8, 48)
+        else:
+            s = np.clip(np.where(rng.integers(0, 2, 48) == 1, 7, 0) + rng.integers(-3, 4, 48), 0, 7)
+        ref = int.from_bytes(bytes(oracle.viterbi_sig(s.astype(np.int8))), "little") & 0x3FFFF
+        assert V.signal_header_bits(s) == ref

@@ -231,3 +231,33 @@ def decode(soft, frame_len, code_rate, guard=True, stats=None):
     if stats is not None:
         stats["carries"] = stats.get("carries", 0) + P.carries
     return np.array(P.out, np.uint8)
+
+
+def signal_header_bits(soft48):
+    """k_signal_vit's SIGNAL decode (zrx_kernels.hip sig_header_bits) on this layout: 24 rate-1/2
+    columns, normalize after 8, 16, 24, pads stored at columns 14 and 22; the 18 header bits
+    (bits 6..23 of Viterbi_sig11's traceback word, viterbicore.hpp:272-315) are the decisions
+    of columns 7..24 along the winner's path: 23, 24 from its newest pad bits, 15..22 and 7..14
+    from the stored pads."""
+    soft48 = np.asarray(soft48, np.int64)
+    P = Packet(3, 0)
+    P.guard = False
+    for c in range(1, 25):
+        P.step5(V3.FULL, int(soft48[2 * c - 2]), int(soft48[2 * c - 1]))
+        if P.tr % 8 == 0:
+            P.normalize()
+    assert P.carries == 0
+    best = None
+    for l in range(NL):
+        for d in range(ND):
+            for h in range(2):
+                half = (int(P.M[l, d]) >> (16 * h)) & 0xFFFF
+                m = ((half >> 7) & 0xFE) | ((half >> 1) & 1)
+                key = (((m << 8) | (4 * int(POS[l, d, h]))) & 0xFFFF) ^ 0x8000   # 24 mod 6 = 0: state = position
+                cand = (key << 16) | (half & 3)
+                best = cand if best is None else min(best, cand)
+    s0, pad = (best >> 18) & 63, best & 3
+    s22 = (s0 >> 2) | ((pad >> 1) << 4) | ((pad & 1) << 5)
+    b22 = int(P.ring[(22 - 6) // 8, s22])
+    b14 = int(P.ring[(14 - 6) // 8, V3.bitrev(b22 & 63, 6)])
+    return b14 | (b22 << 8) | (pad << 16)

@@ -660,7 +660,7 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
                                                                              npkts, (uint4*)c->sig_soft, chan, T);
   if (ev) ZRX_CHECK(hipEventRecord(ev[1], s));
   const bool ordered = order_fits(c, npkts);
-  k_signal_vit<<<blocks(npkts, 4), 256, 0, s>>>(c->sig_soft, d_nsym, npkts, c->cap_nsym, c->vparams, d_info,
+  k_signal_vit<<<blocks(npkts, v3::kRows), 256, 0, s>>>(c->sig_soft, d_nsym, npkts, c->cap_nsym, c->vparams, d_info,
                                                  ordered ? c->nrows : nullptr);
   // A mixed batch's sort and row expansion (k_pkt_rows) only feed the Viterbi, so they can run
   // on a side stream while k_data_fft runs (config 5: -27 us a batch).  The fork and join cost

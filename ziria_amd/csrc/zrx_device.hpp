@@ -274,74 +274,6 @@ __device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
   return v;
 }
 
-// ------------------------------------------------------------------ Viterbi (lane = state)
-// State s = lane.  Predecessors p0 = s>>1 (branch 0, marker 0) and p1 = p0|32 (branch 1,
-// marker 1); input bit x = s&1.  Expected code bits (encoding.blk:92-109):
-// A = x^p1^p2^p4^p5, B = x^p0^p1^p2^p5; branch metric e ? 14-2v : 2v reproduces
-// VIT_MA/VIT_MB (csrc/viterbilut.h:111-285); branch 1 expects the complement bits, so
-// its metric is (28 or 14) - branch 0's.
-struct VitLane {
-  int cA, offA, cB, offB;   // bm0 = cA*2a + offA (+ cB*2b + offB)
-  int src0, src1;           // predecessor lanes
-};
-__device__ __forceinline__ VitLane vit_lane(int s) {
-  const int p0 = s >> 1, x = s & 1;
-  const int A = x ^ ((p0 >> 1) & 1) ^ ((p0 >> 2) & 1) ^ ((p0 >> 4) & 1) ^ ((p0 >> 5) & 1);
-  const int B = x ^ (p0 & 1) ^ ((p0 >> 1) & 1) ^ ((p0 >> 2) & 1) ^ ((p0 >> 5) & 1);
-  VitLane L;
-  L.cA = 1 - 2 * A; L.offA = 14 * A;
-  L.cB = 1 - 2 * B; L.offB = 14 * B;
-  L.src0 = p0; L.src1 = p0 | 32;
-  return L;
-}
-// One trellis column: BranchACS (csrc/viterbicore.hpp:105-147, 241-265, 343-390).
-// USE: 3 = (a on A, b on B), 1 = a on A only, 2 = a on B only.  m holds a u8 metric.
-template <int USE>
-__device__ __forceinline__ uint32_t acs(uint32_t m, int a, int b, const VitLane& L) {
-  const uint32_t m0 = (uint32_t)__shfl((int)m, L.src0);
-  const uint32_t m1 = (uint32_t)__shfl((int)m, L.src1);
-  int bm0, tot;
-  if (USE == 3) { bm0 = L.cA * (2 * a) + L.offA + L.cB * (2 * b) + L.offB; tot = 28; }
-  else if (USE == 1) { bm0 = L.cA * (2 * a) + L.offA; tot = 14; }
-  else { bm0 = L.cB * (2 * a) + L.offB; tot = 14; }
-  const uint32_t r0 = (m0 + (uint32_t)bm0) & 0xFEu;                 // add_epi8, AND 0xFE
-  const uint32_t r1 = ((m1 + (uint32_t)(tot - bm0)) & 0xFFu) | 1u;  // add_epi8, OR 1
-  return min(r0, r1);                                                // min_epu8
-}
-// normalize (csrc/viterbicore.hpp:149-168)
-__device__ __forceinline__ uint32_t vit_normalize(uint32_t m) {
-  return m - (wave_min_u32(m) & 0xFEu);
-}
-// traceback (csrc/viterbicore.hpp:170-239).  Start = argmin of the SIGNED int16 key
-// (m<<8)|(4s) (SSE2 hmin16, :79-96); the state's own survivor bit rides in bit 6.
-// surv(t) returns the 64-bit survivor word of column t (bit s = LSB of m_t[s]).
-// Writes output bytes 0 .. nbits/8-1 (stream order) to out[] from lane 0; any depth.
-template <class SurvRead>
-__device__ __forceinline__ void vit_traceback(uint32_t m, uint32_t col, uint32_t nbits, uint32_t lookahead,
-                                              int lane, SurvRead surv, uint8_t* __restrict__ out) {
-  int key = (int)(int16_t)(uint16_t)((m << 8) | ((uint32_t)lane << 2));
-  key = wave_min_i32(key);
-  uint32_t i = (uint32_t)(key >> 2) & 0x7Fu;
-  uint32_t t = col;
-  for (uint32_t k = 0; k < lookahead; k++) {
-    t--;
-    i = (i >> 1) & 0x3Fu;
-    i |= (uint32_t)((surv(t) >> i) & 1u) << 6;
-  }
-  const int nbytes = (int)(nbits >> 3);
-  for (int byte = nbytes - 1; byte >= 0; byte--) {
-    uint32_t oc = 0;
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      oc = (oc << 1) | ((i >> 6) & 1u);
-      t--;
-      i = (i >> 1) & 0x3Fu;
-      i |= (uint32_t)((surv(t) >> i) & 1u) << 6;
-    }
-    if (lane == 0) out[byte] = (uint8_t)oc;
-  }
-}
-
 // ------------------------------------------------------------------ descrambler / CRC helpers
 // CRC register after processing n zero bytes (linear map), via kCrcZero[k] = 2^k bytes.
 __device__ __forceinline__ uint32_t crc_apply(const uint32_t* M, uint32_t v) {

@@ -3,7 +3,7 @@
 //   k_fft64          one 64-point FFT per lane (FFT<64>, csrc/fft_r4difx.hpp:220-237)
 //   k_signal_fft     SIGNAL symbol per lane: FFT -> GetData -> DemapLimit -> DemapBPSK ->
 //                    DeinterleaveBPSK (DecodePLCP.blk:30-37)
-//   k_signal_vit     one wave per packet: Viterbi_sig11 (viterbicore.hpp:272-315) +
+//   k_signal_vit     one row per packet (v3 layout): Viterbi_sig11 (viterbicore.hpp:272-315) +
 //                    parsePLCPHeader (parsePLCPHeader.blk:119-213)
 //   k_data_fft       lane = data symbol, flat over the batch: FFT -> GetData -> DemapLimit ->
 //                    Demap{mod} -> Deinterleave{mod} (Decode.blk:45-60); with EQ, ChannelEqualization
@@ -23,7 +23,6 @@
 
 namespace zrx {
 
-constexpr int kRing = 512;            // survivor ring columns per packet (>= depth + 64)
 constexpr int kDecStride = 2080;      // decoded bytes per packet in the rx chain (len+2 <= 2050)
 constexpr int kPayloadStride = 4096;  // payload bytes per packet
 
@@ -93,61 +92,68 @@ __global__ __launch_bounds__(256) void k_signal_fft(const uint4* __restrict__ sy
   dst[2] = make_uint4(w[8], w[9], w[10], w[11]);
 }
 
-// ------------------------------------------------------------------ Viterbi core (one wave)
-struct RingLds {
-  uint64_t* r;
-  __device__ __forceinline__ uint64_t operator()(uint32_t t) const { return r[t & (kRing - 1)]; }
-};
-
-// Wave minimum by DPP inside each 16-lane row (xor 1, xor 2, half-row and row mirrors) and
-// four readlanes across rows: no ds_bpermute (the LDS pipe is this kernel's bottleneck).
-template <typename T>
-__device__ __forceinline__ T wave_min_dpp(T v) {
-  v = min(v, (T)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
-  v = min(v, (T)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
-  v = min(v, (T)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));
-  v = min(v, (T)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false));
-  const T a = (T)__builtin_amdgcn_readlane((int)v, 0), b = (T)__builtin_amdgcn_readlane((int)v, 16);
-  const T c = (T)__builtin_amdgcn_readlane((int)v, 32), d = (T)__builtin_amdgcn_readlane((int)v, 48);
-  return min(min(a, b), min(c, d));
+// ------------------------------------------------------------------ SIGNAL Viterbi (rows)
+// Viterbi_sig11 (viterbicore.hpp:272-315) on the data Viterbi's row layout (zrx_viterbi3.hpp:
+// a packet = one kLanes-lane row, v3::kRows packets a block): 24 rate-1/2 columns on the
+// 48 soft values, normalize after columns 8, 16 and 24 (the reference's extra normalize after
+// the loop is then a no-op: the metric minimum is 0 or 1), traceback of 24 bits with lookahead
+// 0 from the key argmin.  parsePLCPHeader keeps bits 6..23 of the traceback word (the >> 6
+// at sora_ext_viterbi.cpp:191), i.e. the decisions of columns 7..24: columns 23, 24 are the
+// winner's newest pad bits, 15..22 and 7..14 the pad bytes stored at columns 22 and 14 (the
+// column with cycle phase 7) along its path.  So a packet costs 24 packed columns of one row,
+// two snapshots and two dependent LDS reads (tests/vit8_model.py signal_header_bits restates it).
+// Rate-1/2 columns never wrap the u8 metric (zrx_viterbi3.hpp "Guard-free columns": the
+// initial 0 / 48 metrics included), so they run without the guard.
+__device__ __forceinline__ uint32_t sig_soft_byte(const uint32_t (&sw)[12], int i) {
+  return sw[i >> 2] >> (8 * (i & 3));
 }
-
-// Viterbi_sig11 (viterbicore.hpp:272-315): 24 full steps on 48 soft values held as 12 dwords
-// in lanes 0..11 of `dw`, normalize every 8 steps and once more at the end, traceback of 24
-// bits with lookahead 0 (viterbicore.hpp:170-239).  The 24 survivor words (ballots of the
-// metric LSBs) stay in SGPRs and the traceback runs on the scalar unit.  Returns the three
-// traceback bytes, byte 0 lowest (before the brick's >> 6 at sora_ext_viterbi.cpp:191).
-__device__ __forceinline__ uint32_t sig11_word(uint32_t dw, int lane) {
-  const VitLane L = vit_lane(lane);
-  uint32_t m = lane == 0 ? 0u : 48u;
-  uint64_t surv[24];
-  surv[0] = 0;                                         // column 0: no markers
+template <int J>
+__device__ __forceinline__ void sig_col(uint32_t (&M)[v3::kDw], const v3::Consts& K, const uint32_t (&sw)[12],
+                                        uint8_t (*snap)[64], uint32_t l) {
+  const uint32_t P = v3::p_word(v3::p_kind(0), sig_soft_byte(sw, 2 * J), sig_soft_byte(sw, 2 * J + 1));
+  v3::column5<J % 6, 0, (J + 2) % 8, false>(M, P, K);
+  constexpr int c = J + 1;                             // columns done
+  if constexpr (c % 8 == 0) v3::normalize(M);
+  if constexpr (c == 14 || c == 22) {                  // pad bytes by state (position p: rotl6(p, c))
 #pragma unroll
-  for (int t = 1; t <= 24; t++) {
-    const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)dw, (2 * t - 2) >> 2);
-    const int sh = ((2 * t - 2) & 3) * 8;
-    const int a = (word >> sh) & 0xFF, b = (word >> (sh + 8)) & 0xFF;
-    m = acs<3>(m, a, b, L);
-    if ((t & 7) == 0) m -= wave_min_dpp<uint32_t>(m) & 0xFEu;
-    if (t < 24) surv[t] = __ballot((m & 1u) != 0);
+    for (int q = 0; q < 2 * v3::kDw; q++)
+      snap[c == 22][v3::rotl6(v3::pos_of(l, q >> 1, q & 1), c % 6)] = (uint8_t)(M[q >> 1] >> (16 * (q & 1)));
   }
-  m -= wave_min_dpp<uint32_t>(m) & 0xFEu;
-  const int key = wave_min_dpp<int>((int)(int16_t)(uint16_t)((m << 8) | ((uint32_t)lane << 2)));
-  uint32_t i = (uint32_t)__builtin_amdgcn_readfirstlane((key >> 2) & 0x7F);
-  uint32_t word = 0;
+}
+template <int... J>
+__device__ __forceinline__ void sig_cols(uint32_t (&M)[v3::kDw], const v3::Consts& K, const uint32_t (&sw)[12],
+                                         uint8_t (*snap)[64], uint32_t l, std::integer_sequence<int, J...>) {
+  (sig_col<J>(M, K, sw, snap, l), ...);
+}
+// The 18 header bits (bits 6..23 of the sig11 traceback word) of the row's packet.
+__device__ __forceinline__ uint32_t sig_header_bits(const uint32_t (&sw)[12], uint32_t l, uint8_t (*snap)[64]) {
+  v3::Consts K;
+  v3::make_consts(K, l, 0);
+  uint32_t M[v3::kDw];
 #pragma unroll
-  for (int byte = 2; byte >= 0; byte--) {
-    uint32_t oc = 0;
+  for (int d = 0; d < v3::kDw; d++)                    // H = 0 at state 0, 48 elsewhere (halved, bits 14..8)
+    M[d] = (v3::pos_of(l, d, 0) ? 24u << 8 : 0u) | ((v3::pos_of(l, d, 1) ? 24u << 8 : 0u) << 16);
+  sig_cols(M, K, sw, snap, l, std::make_integer_sequence<int, 24>{});
+  // argmin of the signed int16 key (m << 8) | 4s at column 24 (24 mod 6 = 0: state = position),
+  // m = the reference's metric: H | the marker of column 24 (pad bit 1)
+  uint32_t best = 0xFFFFFFFFu;
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-      const int t = 8 * byte + 7 - j;                  // column read by this step
-      oc = (oc << 1) | ((i >> 6) & 1u);
-      i = (i >> 1) & 0x3Fu;
-      i |= (uint32_t)((surv[t] >> i) & 1u) << 6;
-    }
-    word |= oc << (8 * byte);
+  for (int q = 0; q < 2 * v3::kDw; q++) {
+    const uint32_t half = (M[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
+    const uint32_t m = ((half >> 7) & 0xFEu) | ((half >> 1) & 1u);
+    const uint32_t ukey = (((m << 8) | (v3::pos_of(l, q >> 1, q & 1) << 2)) & 0xFFFFu) ^ 0x8000u;
+    best = min(best, (ukey << 16) | (half & 3u));
   }
-  return word;
+  best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0xB1, 0xF, 0xF, false));
+  best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x4E, 0xF, 0xF, false));
+  if constexpr (v3::kLanes >= 8) best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x141, 0xF, 0xF, false));
+  if constexpr (v3::kLanes == 16) best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x140, 0xF, 0xF, false));
+  const uint32_t s0 = (best >> 18) & 63u, pad = best & 3u;   // pad bit 0: column 23, bit 1: column 24
+  // state at column 22: its bits 0..3 = s0 bits 2..5, bit 4 = decision 24, bit 5 = decision 23
+  const uint32_t s22 = (s0 >> 2) | ((pad >> 1) << 4) | ((pad & 1u) << 5);
+  const uint32_t b22 = snap[1][s22];                   // decisions of columns 15..22 (bit j: 15 + j)
+  const uint32_t b14 = snap[0][v3::rev6(b22 & 63u)];   // columns 7..14; state at 14 = rev6(decisions 15..20)
+  return b14 | (b22 << 8) | (pad << 16);
 }
 
 __device__ __forceinline__ int ncbps_of(int mod) { return mod == 0 ? 48 : mod == 1 ? 96 : mod == 2 ? 192 : 288; }
@@ -167,11 +173,16 @@ __device__ __forceinline__ int ndbps_of(int mod, int coding) {
 __global__ __launch_bounds__(256) void k_signal_vit(const uint32_t* __restrict__ sig_soft, const int32_t* __restrict__ nsym,
                                                     int npkts, int cap_nsym, int32_t* __restrict__ vparams,
                                                     int32_t* __restrict__ info, int32_t* plan) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int p = blockIdx.x * 4 + wv;
+  __shared__ uint8_t snap[v3::kRows][2][64];           // [row][column 14, 22][state]
+  const uint32_t l = threadIdx.x & (v3::kLanes - 1u), r = threadIdx.x >> v3::kLaneBits;
+  const int wave0 = blockIdx.x * v3::kRows + (int)((threadIdx.x >> 6) * v3::kRowsWave);
+  if (wave0 >= npkts) return;                          // (wave-uniform)
+  const int p = blockIdx.x * v3::kRows + (int)r;
+  const uint4* src = (const uint4*)(sig_soft + (int64_t)min(p, npkts - 1) * 12);
+  const uint4 q0 = src[0], q1 = src[1], q2 = src[2];
+  const uint32_t sw[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+  const uint32_t hb = sig_header_bits(sw, l, snap[r]);
   if (p >= npkts) return;
-  const uint32_t dw = lane < 12 ? sig_soft[(int64_t)p * 12 + lane] : 0u;
-  const uint32_t hb = (sig11_word(dw, lane) >> 6) & 0x3FFFFu;   // bits 18..23 := 0
   // parsePLCPHeader.blk:124-158 RATE nibble (bit k of the nibble = hdata[k])
   int mod = 0, cod = 0;
   switch (hb & 0xF) {
@@ -195,7 +206,7 @@ __global__ __launch_bounds__(256) void k_signal_vit(const uint32_t* __restrict__
   if (err) status = 1;
   else if (need > nsym[p] - 1) status = 2;
   else if (need > cap_nsym - 1) status = 3;
-  if (lane == 0) {
+  if (l == 0) {
     int32_t* vp = vparams + 4 * (int64_t)p;
     vp[0] = len + 2;                                  // Decode.blk:59 Viterbi(h.coding, h.len+2)
     vp[1] = cod;
