@@ -9,7 +9,8 @@ from collections import defaultdict
 sys.path.insert(0, ".")
 from ziria_amd.build import source_hash  # noqa: E402
 
-KERNELS = {"k_viterbi3<0, false>": "k_viterbi3", "k_data_fft<false>": "k_data_fft"}
+KERNELS = {"k_viterbi3<0, false>": "k_viterbi3", "k_data_fft<false>": "k_data_fft", "k_descramble_crc": "k_descramble_crc",
+           "k_signal_vit": "k_signal_vit", "k_signal_fft<false>": "k_signal_fft", "k_pkt_plan": "k_pkt_plan"}
 vals = defaultdict(lambda: defaultdict(list))
 for i in (11, 12):
     for r in csv.DictReader(open(f"gpurun_out/pmc{i}/pmc_counter_collection.csv")):

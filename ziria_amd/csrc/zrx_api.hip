@@ -136,6 +136,7 @@ static inline int blocks(int64_t n, int per) { return (int)((n + per - 1) / per)
 #define ZRX_SIGFFT_LANES 64
 #endif
 constexpr int kSigFftLanes = ZRX_SIGFFT_LANES;
+static_assert(kSigFftLanes % 64 == 0, "k_signal_fft stages its LUT with 64-thread strides");
 
 // Trig tables of ChannelEqualization / PilotTrack: the reference LUTs (csrc/intalglutx.h:23,
 // :3667, :7351) in closed form, with pi written as 3.141593 as their generator did:

@@ -55,8 +55,15 @@ __device__ __forceinline__ void load_symbol(const uint4* __restrict__ src, s2* x
   }
 }
 
+// (blocks of a multiple of 64 threads: every load issued before the first store, one memory
+// latency; a strided loop over blockDim waited for each of its rounds in turn)
 __device__ __forceinline__ void stage_lut(uint32_t* lut) {
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) lut[i] = kDemapLut[i];
+  const uint32_t t = threadIdx.x & 63u;
+  uint32_t v[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) v[k] = kDemapLut[t + 64 * k];
+#pragma unroll
+  for (int k = 0; k < 4; k++) lut[t + 64 * k] = v[k];
   __syncthreads();
 }
 
@@ -654,8 +661,13 @@ __global__ __launch_bounds__(256) void k_data_fft(const uint4* __restrict__ sym,
                                                   const int32_t* __restrict__ dsym, const int32_t* __restrict__ wave_p0,
                                                   const uint32_t* __restrict__ chan, EqTabs T) {
   __shared__ uint4 stage_all[kDfWaves][kDfUnits > 0 ? kDfUnits : 1];
-  __shared__ uint32_t lut_all[256 * kDfLutCopies];
-  for (int i = threadIdx.x; i < 256 * kDfLutCopies; i += blockDim.x) lut_all[i] = kDemapLut[i / kDfLutCopies];
+  __shared__ uint4 lut_all4[256];                     // kDfLutCopies (4) copies of entry i at 4i ..
+  static_assert(kDfLutCopies == 4, "one uint4 per LUT entry");
+  {
+    const uint32_t v = kDemapLut[threadIdx.x];         // (256 threads: one entry each, one latency)
+    lut_all4[threadIdx.x] = make_uint4(v, v, v, v);
+  }
+  const uint32_t* lut_all = (const uint32_t*)lut_all4;
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -792,11 +804,21 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
   __shared__ uint32_t shf[16][128];                   // [n]: n * 32 zero bytes, [8 + n]: n * 256
   __shared__ uint32_t scrw[128];
   __shared__ uint8_t scrb[256];
-  for (int i = threadIdx.x; i < 1024; i += blockDim.x) s4[i >> 8][i & 255] = kCrcS4[i >> 8][i & 255];
-  for (int i = threadIdx.x; i < 1024; i += blockDim.x) shf[i >> 7][i & 127] = kCrcShiftLo[i >> 7][i & 127];
-  for (int i = threadIdx.x; i < 1024; i += blockDim.x) shf[8 + (i >> 7)][i & 127] = kCrcShiftHi[i >> 7][i & 127];
-  for (int i = threadIdx.x; i < 254; i += blockDim.x) scrb[i] = kScrB2[i];
-  for (int i = threadIdx.x; i < 127; i += blockDim.x) scrw[i] = kScrW[i];
+  {                                                    // every table load in flight at once
+    static_assert(64 * kCrcWaves == 512, "two words of each 1024-word table per thread");
+    const int t = threadIdx.x;
+    const uint32_t* S4 = &kCrcS4[0][0];
+    const uint32_t* SL = &kCrcShiftLo[0][0];
+    const uint32_t* SH = &kCrcShiftHi[0][0];
+    const uint32_t a0 = S4[t], a1 = S4[t + 512], b0 = SL[t], b1 = SL[t + 512], c0 = SH[t], c1 = SH[t + 512];
+    const uint32_t d = kScrW[min(t, 126)];
+    const uint8_t e = kScrB2[min(t, 253)];
+    (&s4[0][0])[t] = a0; (&s4[0][0])[t + 512] = a1;
+    (&shf[0][0])[t] = b0; (&shf[0][0])[t + 512] = b1;
+    (&shf[8][0])[t] = c0; (&shf[8][0])[t + 512] = c1;
+    if (t < 127) scrw[t] = d;
+    if (t < 254) scrb[t] = e;
+  }
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // (packet values below: scalar)
