@@ -564,37 +564,18 @@ __global__ __launch_bounds__(1024) void k_pkt_rows(const int32_t* __restrict__ v
 }
 
 // ---- k_data_fft: FFT64 + GetData + DemapLimit + Demap + Deinterleave, lane = data symbol ----
-// The FFT runs one symbol per lane (no cross-lane traffic), but a lane's 256-B symbol and its
-// 288-B soft row are a poor memory pattern: 64 rows per load or store instruction.  Each wave
-// can move its 64 symbols through its own LDS region (ZRX_DF_IN / ZRX_DF_OUT select, for A/B):
-//  * in (DF_IN 1, 2): 16 LDS-DMA loads (global_load_lds_dwordx4), each 1 KiB of 4 whole
-//    symbols.  The destination of a DMA load is lane-linear, so the skew sits on the source:
-//    LDS unit 16s + ((c + s) mod 16) holds 16-B chunk c of symbol s, and lane s's 16
-//    ds_read_b128 of chunk c land on 16 distinct 16-B slots in every lane group.  DF_IN 2
-//    issues the next iteration's loads as soon as this one's symbols are in registers.
-//  * out (DF_OUT 1): the demapper writes unit q of the soft row to 19s + q (stride 19: the
-//    8-lane groups of ds_write_b128 hit 8 slots), then 18 store instructions each take 64
-//    consecutive units of the wave's rows, (s, q) = divmod(64j + lane, 18): 1 KiB runs.
-// DF_IN 0 / DF_OUT 0: each lane loads / stores its own row (16 / 18 x 16 B).
-// A wave never waits on another: LDS is in order within a wave, so there are no barriers.
-#ifndef ZRX_DF_IN
-#define ZRX_DF_IN 0
-#endif
-#ifndef ZRX_DF_OUT
-#define ZRX_DF_OUT 1
-#endif
-constexpr int kDfIn = ZRX_DF_IN, kDfOut = ZRX_DF_OUT;
+// The FFT runs one symbol per lane (no cross-lane traffic).  A lane's 288-B soft row is a poor
+// store pattern (64 rows per store instruction), so each wave moves its rows through its own
+// LDS region: the demapper writes unit q of the soft row to 19s + q (stride 19: the 8-lane
+// groups of ds_write_b128 hit 8 slots), then 18 store instructions each take 64 consecutive
+// units of the wave's rows, (s, q) = divmod(64j + lane, 18): 1 KiB runs.  A wave never waits
+// on another: LDS is in order within a wave, so there are no barriers.  (Tried and dropped,
+// symbol loads by LDS-DMA, with and without a one-iteration prefetch; soft rows
+// stored by each lane.)
 constexpr int kDfWaves = 4;           // waves per block
 constexpr int kDfRow = 19;            // output staging row stride, 16-B units (a soft row is <= 18)
-constexpr int kDfInUnits = kDfIn ? 1024 : 0;
-constexpr int kDfOutUnits = kDfOut ? 64 * kDfRow : 0;
-// one region per wave: input and output share it unless the input is prefetched
-constexpr int kDfUnits = kDfIn == 2 ? kDfInUnits + kDfOutUnits : (kDfInUnits > kDfOutUnits ? kDfInUnits : kDfOutUnits);
-constexpr int kDfOutBase = kDfIn == 2 ? kDfInUnits : 0;
+constexpr int kDfUnits = 64 * kDfRow;
 constexpr int kDfLutCopies = 4;       // demap LUT copies (lane & 3): fewer LDS bank conflicts
-constexpr int kDfLdsBytes = kDfWaves * kDfUnits * 16 + 256 * kDfLutCopies * 4;
-constexpr int kDfBlocksPerCu = kDfLdsBytes == 0 ? 4 : (160 * 1024) / kDfLdsBytes < 1 ? 1
-                             : (160 * 1024) / kDfLdsBytes > 4 ? 4 : (160 * 1024) / kDfLdsBytes;
 
 __device__ __forceinline__ int soft_units_of(int mod) { return mod == 0 ? 3 : mod == 1 ? 6 : mod == 2 ? 12 : 18; }
 
@@ -612,42 +593,51 @@ struct DfSym {
   int p, k, mod;
   uint32_t sidx, nu, obase;   // obase: soft row in 16-B units
 };
-__device__ __forceinline__ DfSym df_sym(int w, int lane, int total, const int64_t* __restrict__ sym_off,
-                                        const int32_t* __restrict__ vparams, const int64_t* __restrict__ soft_off,
-                                        const int32_t* __restrict__ dsym, const int32_t* __restrict__ wave_p0) {
-  DfSym d;
+// Where the lane's symbol g = 64w + lane sits (k_pkt_plan's numbering), from wave-uniform
+// scalar loads: the wave's first packet wave_p0[w], then the packet boundaries dsym[q + 1 ..
+// q + 8] eight at a time until a block passes the wave's last symbol (one block unless the
+// wave spans more than 8 packets).  The per-lane loads of the packet's parameters are only
+// issued here (df_finish waits for them), so the next wave's lookup runs under this one's FFT.
+struct DfNext {
+  bool valid;
+  int p, k, mod;
+  int64_t soff, ooff;
+};
+__device__ __forceinline__ void df_locate(int w, int lane, int total, int npkts, const int64_t* __restrict__ sym_off,
+                                          const int32_t* __restrict__ vparams, const int64_t* __restrict__ soft_off,
+                                          const int32_t* __restrict__ dsym, const int32_t* __restrict__ wave_p0,
+                                          DfNext& n) {
   const int g = w * 64 + lane;
-  d.valid = g < total;
-  int p = wave_p0[w];
-  if (d.valid)
-    while (dsym[p + 1] <= g) p++;                    // packets of fewer than 64 symbols
-  d.p = p;
-  d.k = g - dsym[p];
-  d.mod = d.valid ? vparams[4 * (int64_t)p + 3] : 0;
-  d.sidx = d.valid ? (uint32_t)(sym_off[p] + 1 + d.k) : 0u;
-  d.nu = d.valid ? (uint32_t)soft_units_of(d.mod) : 0u;
-  d.obase = d.valid ? (uint32_t)(soft_off[p] / 16) + (uint32_t)d.k * d.nu : 0u;
+  n.valid = g < total;
+  int q = __builtin_amdgcn_readfirstlane(wave_p0[w]);
+  int p = q, base = dsym[q];
+  const int glast = w * 64 + 63;
+  for (;;) {
+    int b[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) b[j] = dsym[min(q + 1 + j, npkts)];   // (dsym[npkts] = total)
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+      if (b[j] <= g) { p = q + 1 + j; base = b[j]; }
+    if (b[7] > glast || q + 8 >= npkts) break;
+    q += 8;
+  }
+  n.p = p;
+  n.k = g - base;
+  n.mod = n.valid ? vparams[4 * (int64_t)p + 3] : 0;
+  n.soff = n.valid ? sym_off[p] : 0;
+  n.ooff = n.valid ? soft_off[p] : 0;
+}
+__device__ __forceinline__ DfSym df_finish(const DfNext& n) {
+  DfSym d;
+  d.valid = n.valid;
+  d.p = n.p;
+  d.k = n.k;
+  d.mod = n.mod;
+  d.sidx = n.valid ? (uint32_t)(n.soff + 1 + n.k) : 0u;
+  d.nu = n.valid ? (uint32_t)soft_units_of(n.mod) : 0u;
+  d.obase = n.valid ? (uint32_t)(n.ooff / 16) + (uint32_t)n.k * d.nu : 0u;
   return d;
-}
-// 16 LDS-DMA loads of wave w's symbols into buf (1 KiB each; chunk c of symbol s at unit
-// 16s + ((c + s) & 15))
-__device__ __forceinline__ void df_load_lds(const char* symb, uint4* buf, const DfSym& d, int w, int total, int lane) {
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    const int s = 4 * i + (lane >> 4);
-    const uint32_t si = (uint32_t)__shfl((int)d.sidx, s);
-    const int c = ((lane & 15) - s) & 15;
-    if (w * 64 + s < total)
-      __builtin_amdgcn_global_load_lds((const void*)(symb + (size_t)si * 256 + 16 * c),
-                                       (__attribute__((address_space(3))) void*)(buf + 64 * i), 16, 0, 0);
-  }
-}
-__device__ __forceinline__ void df_read_lds(const uint4* buf, int lane, s2* x) {
-#pragma unroll
-  for (int c = 0; c < 16; c++) {
-    const uint4 v = buf[16 * lane + ((c + lane) & 15)];
-    x[4 * c] = as_s2(v.x); x[4 * c + 1] = as_s2(v.y); x[4 * c + 2] = as_s2(v.z); x[4 * c + 3] = as_s2(v.w);
-  }
 }
 
 // Flat over the batch's data symbols (k_pkt_plan numbers them): wave w takes symbols
@@ -660,7 +650,7 @@ __global__ __launch_bounds__(256) void k_data_fft(const uint4* __restrict__ sym,
                                                   uint4* __restrict__ soft, const int64_t* __restrict__ soft_off,
                                                   const int32_t* __restrict__ dsym, const int32_t* __restrict__ wave_p0,
                                                   const uint32_t* __restrict__ chan, EqTabs T) {
-  __shared__ uint4 stage_all[kDfWaves][kDfUnits > 0 ? kDfUnits : 1];
+  __shared__ uint4 stage_all[kDfWaves][kDfUnits];
   __shared__ uint4 lut_all4[256];                     // kDfLutCopies (4) copies of entry i at 4i ..
   static_assert(kDfLutCopies == 4, "one uint4 per LUT entry");
   {
@@ -673,78 +663,50 @@ __global__ __launch_bounds__(256) void k_data_fft(const uint4* __restrict__ sym,
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint4* stage = stage_all[wv];
   const uint32_t* lut = lut_all + (lane & (kDfLutCopies - 1));
-  const char* symb = (const char*)sym;
   const int total = dsym[npkts];
   const int nw = (total + 63) >> 6;
   const int wstep = gridDim.x * kDfWaves;
   int w = __builtin_amdgcn_readfirstlane(blockIdx.x * kDfWaves + wv);
   DfSym d;
   if (w < nw) {
-    d = df_sym(w, lane, total, sym_off, vparams, soft_off, dsym, wave_p0);
-    if constexpr (kDfIn == 2) df_load_lds(symb, stage, d, w, total, lane);
+    DfNext n;
+    df_locate(w, lane, total, npkts, sym_off, vparams, soft_off, dsym, wave_p0, n);
+    d = df_finish(n);
   }
   for (; w < nw; w += wstep) {
     s2 x[64];
-    if constexpr (kDfIn == 0) {
-      load_symbol(sym + (size_t)d.sidx * 16, x);
-    } else {
-      if constexpr (kDfIn == 1) df_load_lds(symb, stage, d, w, total, lane);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      df_read_lds(stage, lane, x);
-    }
-    // DF_IN 2: the next iteration's symbols are located and their loads issued now (every
-    // lane has read its input above before the DMA overwrites it)
+    load_symbol(sym + (size_t)d.sidx * 16, x);
     const int wn = w + wstep;
-    DfSym dn;
-    if constexpr (kDfIn == 2) {
-      if (wn < nw) {
-        dn = df_sym(wn, lane, total, sym_off, vparams, soft_off, dsym, wave_p0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        df_load_lds(symb, stage, dn, wn, total, lane);
-      }
-    }
+    DfNext n;
+    if (wn < nw) df_locate(wn, lane, total, npkts, sym_off, vparams, soft_off, dsym, wave_p0, n);
     // ---- compute
     const uint32_t* cp = EQ ? chan + (int64_t)d.p * 64 : nullptr;
     if (d.valid) {
-      if constexpr (kDfOut == 1) {
-        uint4* row = stage + kDfOutBase + kDfRow * lane;
-        auto st = [row](int q, uint4 v) { row[q] = v; };
-        switch (d.mod) {
-          case 0: data_fft_symbol<0, EQ>(x, d.k, lut, st, cp, T); break;
-          case 1: data_fft_symbol<1, EQ>(x, d.k, lut, st, cp, T); break;
-          case 2: data_fft_symbol<2, EQ>(x, d.k, lut, st, cp, T); break;
-          default: data_fft_symbol<3, EQ>(x, d.k, lut, st, cp, T); break;
-        }
-      } else {
-        uint4* row = soft + d.obase;
-        auto st = [row](int q, uint4 v) { row[q] = v; };
-        switch (d.mod) {
-          case 0: data_fft_symbol<0, EQ>(x, d.k, lut, st, cp, T); break;
-          case 1: data_fft_symbol<1, EQ>(x, d.k, lut, st, cp, T); break;
-          case 2: data_fft_symbol<2, EQ>(x, d.k, lut, st, cp, T); break;
-          default: data_fft_symbol<3, EQ>(x, d.k, lut, st, cp, T); break;
-        }
+      uint4* row = stage + kDfRow * lane;
+      auto st = [row](int q, uint4 v) { row[q] = v; };
+      switch (d.mod) {
+        case 0: data_fft_symbol<0, EQ>(x, d.k, lut, st, cp, T); break;
+        case 1: data_fft_symbol<1, EQ>(x, d.k, lut, st, cp, T); break;
+        case 2: data_fft_symbol<2, EQ>(x, d.k, lut, st, cp, T); break;
+        default: data_fft_symbol<3, EQ>(x, d.k, lut, st, cp, T); break;
       }
     }
-    if constexpr (kDfOut == 1) {
-      __builtin_amdgcn_wave_barrier();
-      // ---- out: 18 x 64 units, (s, q) = divmod(64j + lane, 18)
-      // (lane0 is lane through an opaque move: the divmods are recomputed here each time
-      // instead of being hoisted out of the loop as 54 live registers)
-      int lane0;
-      asm volatile("v_mov_b32 %0, %1" : "=v"(lane0) : "v"(lane));
+    __builtin_amdgcn_wave_barrier();
+    // ---- out: 18 x 64 units, (s, q) = divmod(64j + lane, 18)
+    // (lane0 is lane through an opaque move: the divmods are recomputed here each time
+    // instead of being hoisted out of the loop as 54 live registers)
+    int lane0;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(lane0) : "v"(lane));
 #pragma unroll
-      for (int j = 0; j < 18; j++) {
-        const int u = 64 * j + lane0;
-        const int s = u / 18, q = u - 18 * s;
-        const uint32_t o = (uint32_t)__shfl((int)d.obase, s), n = (uint32_t)__shfl((int)d.nu, s);
-        const uint4 v = stage[kDfOutBase + kDfRow * s + q];
-        if ((uint32_t)q < n) soft[o + q] = v;
-      }
-      __builtin_amdgcn_wave_barrier();
+    for (int j = 0; j < 18; j++) {
+      const int u = 64 * j + lane0;
+      const int s = u / 18, q = u - 18 * s;
+      const uint32_t o = (uint32_t)__shfl((int)d.obase, s), nu = (uint32_t)__shfl((int)d.nu, s);
+      const uint4 v = stage[kDfRow * s + q];
+      if ((uint32_t)q < nu) soft[o + q] = v;
     }
-    if constexpr (kDfIn == 2) d = dn;
-    else if (wn < nw) d = df_sym(wn, lane, total, sym_off, vparams, soft_off, dsym, wave_p0);
+    __builtin_amdgcn_wave_barrier();
+    if (wn < nw) d = df_finish(n);
   }
 }
 
