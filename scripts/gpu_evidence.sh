@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 evidence run: GPU parity suite, smoke, the driver's bench command, rocprof kernel
+# Evidence run: GPU parity suite, smoke, the driver's bench command, rocprof kernel
 # stats + PMC passes (scripts/gpu_pmc.sh), the config-4 strong-scaling shard sizes, the other
 # BASELINE configs and §8f rows, the host-sanitized driver's GPU tests, the per-call bench.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"

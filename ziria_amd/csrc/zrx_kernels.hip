@@ -334,8 +334,7 @@ __device__ __forceinline__ void plan_rows_mixed(const int32_t* __restrict__ vpar
   // the second writes the rows there.  (Sorted by rate first, the blocks' lengths rise and
   // fall three times, and the snake over that order paired long blocks with long ones: config
   // 5's per-SIMD columns spread 768..11 614 around a mean of 9026.)
-  // (ranked units: kPlanUnit rows — a wave's 8 for the dynamic queue of kDynMixed, else a
-  // block's 32 placed over the CUs)
+  // (ranked units: kPlanUnit rows, a block's 32, placed over the CUs)
   const uint32_t total = *rtotal, nfull = total / (uint32_t)v3::kPlanUnit;
   const uint32_t ncu2 = (uint32_t)max(ncu, 2), ncu_rcp = 0xFFFFFFFFu / ncu2 + 1u;
   const bool ranked = ZRX_RANK_BLOCKS && nfull <= (uint32_t)v3::kRankBlocks;
@@ -374,7 +373,7 @@ __device__ __forceinline__ void plan_rows_mixed(const int32_t* __restrict__ vpar
         } else {
           for (uint32_t k = 0; k < ns[i]; k++) {
             const uint32_t pos = ex + k, b = pos / (uint32_t)v3::kPlanUnit;
-            const uint32_t at = !ranked ? (v3::kDynMixed ? pos : v3::order_place(pos, nfull, ncu2, ncu_rcp))
+            const uint32_t at = !ranked ? v3::order_place(pos, nfull, ncu2, ncu_rcp)
                                 : b < nfull ? blk[b] * (uint32_t)v3::kPlanUnit + pos % (uint32_t)v3::kPlanUnit : pos;
             if (at < (uint32_t)rows_cap) rows[at] = make_int2(pk[i], (int)(k | (ns[i] << 8)));   // (always: the plan's row bound)
           }
@@ -402,7 +401,7 @@ __device__ __forceinline__ void plan_rows_mixed(const int32_t* __restrict__ vpar
         const uint32_t key = b < nfull ? (uint32_t)kOrderLen - 1u - min((blk[b] + 23u) / 24u, (uint32_t)kOrderLen - 1u) : 0u;
         const uint32_t r = order_claim(hist, b < nfull, key);
         __syncthreads();                               // every lane read blk[] before it is rewritten
-        if (b < nfull) blk[b] = v3::kDynMixed ? r : v3::rank_place(r, nfull, ncu2, ncu_rcp);   // (queue: rank order)
+        if (b < nfull) blk[b] = v3::rank_place(r, nfull, ncu2, ncu_rcp);
       }
       __syncthreads();
     }
@@ -415,7 +414,6 @@ __device__ __forceinline__ void plan_rows_mixed(const int32_t* __restrict__ vpar
     // bound must show (zrx_plan_check) instead of leaving packets silently undecoded
     nrows[v3::kPlanDropped] = total > (uint32_t)rows_cap ? (int32_t)(total - (uint32_t)rows_cap) : 0;
     nrows[v3::kPlanNcu] = (int32_t)ncu2;
-    nrows[v3::kPlanQueue] = 0;                         // (kDynMixed: the tasks' queue word)
   }
 }
 

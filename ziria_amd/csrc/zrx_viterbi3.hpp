@@ -395,20 +395,8 @@ __host__ __device__ __forceinline__ uint32_t rank_place(uint32_t r, uint32_t nfu
 // batch equal in all of it reuses the plan (k_pkt_plan returns at once).
 enum PlanWord { kPlanRows = 0, kPlanFixes = 1, kPlanUniform = 2, kPlanNcu = 3, kPlanSegLen = 4, kPlanDropped = 5,
                 kPlanExpN = 8, kPlanExpLen = 9, kPlanExpCr = 10, kPlanExpSoft = 11, kPlanExpMod = 12,
-                kPlanMismatch = 13, kPlanQueue = 14, kPlanWords = 16 };
-// A mixed batch's Viterbi (kDynMixed): persistent waves, two blocks per CU, pull 8-row tasks
-// (one wave's rows) from the queue word kPlanQueue in the plan's order, which ranks the tasks
-// by their longest row, longest first (LPT): a wave that finishes early takes the next task,
-// so no block waits for a CU a whole block-length late.  0: the static ranked block placement
-// of round 3 (rank_place).
-#ifndef ZRX_DYN_MIXED
-#define ZRX_DYN_MIXED 0
-#endif
-constexpr bool kDynMixed = ZRX_DYN_MIXED != 0;
-#ifndef ZRX_DYN_PRIO
-#define ZRX_DYN_PRIO 1   // (the younger-wave issue priority for the queue's waves too)
-#endif
-constexpr int kPlanUnit = kDynMixed ? kRowsWave : kRows;   // rows ranked together by the mixed plan
+                kPlanMismatch = 13, kPlanWords = 16 };
+constexpr int kPlanUnit = kRows;                       // rows ranked together by the mixed plan (a block's)
 
 // start unit m_k of segment k >= 1 of nseg over a frame of E = 8 len + 6 columns (rounded
 // k E / nseg; with E / nseg >= kMinCut the m_k are distinct (steps of > 1 unit) and
@@ -1377,8 +1365,7 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
         // younger wave's 2 of 3 bodies otherwise
         const bool mixed = rows != nullptr && uni == 0u;
         const bool lrpt = !FIX && (v3::kPrioMode == 2 || (v3::kPrioMode == 3 && mixed));
-        const bool younger = !FIX && (v3::kPrioMode == 1 || (v3::kPrioMode == 3 && !mixed)) && ((blockIdx.x / ncu) & 1u) != 0u &&
-                             !(v3::kDynMixed && mixed && !ZRX_DYN_PRIO);
+        const bool younger = !FIX && (v3::kPrioMode == 1 || (v3::kPrioMode == 3 && !mixed)) && ((blockIdx.x / ncu) & 1u) != 0u;
         v3::Row Rr;
         Rr.ob = xfix ? v3::kSegWarm - v3::kSegCmp : xk ? v3::kSegWarm : 0u;
         Rr.end = x.E - x.S; Rr.cols = colsS;
@@ -1437,21 +1424,6 @@ __global__ __launch_bounds__(256, v3::kWavesPerSimd) void k_viterbi3(const uint8
     for (int g0 = blockIdx.x * v3::kRows; g0 < nrows; g0 += gridDim.x * v3::kRows)
       viterbi_rows<DBG, true>(g0, nrows, uni, ncu, ncu_rcp, K, ring, rowx, soft, soft_off, vparams, out, out_off, out_bits, rows, segs, dumps,
                               nrows_p);
-  } else if (v3::kDynMixed && rows && uni == 0u) {
-    // a mixed batch: each wave of the first 2 ncu blocks (those resident at once) pulls 8-row
-    // tasks, longest first, until the queue is empty (every wave reaches the exit)
-    if (blockIdx.x >= 2u * ncu) return;
-    const int wib = (int)(threadIdx.x >> 6);
-    const uint32_t ntasks = ((uint32_t)nrows + v3::kRowsWave - 1u) / v3::kRowsWave;
-    for (;;) {
-      uint32_t task = 0;
-      if ((threadIdx.x & 63u) == 0u) task = atomicAdd((uint32_t*)(nrows_p + v3::kPlanQueue), 1u);
-      task = (uint32_t)__builtin_amdgcn_readfirstlane((int)task);
-      if (task >= ntasks) break;
-      // (row slot = g0 + row-in-block: this wave's rows are task x 8 .. + 7)
-      viterbi_rows<DBG, false>((int)(task * v3::kRowsWave) - wib * v3::kRowsWave, nrows, uni, ncu, ncu_rcp, K, ring, rowx,
-                               soft, soft_off, vparams, out, out_off, out_bits, rows, segs, dumps, nullptr);
-    }
   } else {
     const int g0 = blockIdx.x * v3::kRows;
     if (g0 < nrows)
