@@ -78,7 +78,7 @@ def main():
                     help="batches in flight: 2 = two engines (own workspace and stream) take the steps in "
                          "turn, as a streaming receiver would, so one batch's tail overlaps the next one's head; "
                          "0 (default) = auto: 2 for an rx batch under %d packets per GPU (zrx_pipeline_link "
-                         "mode 1) and for configs 2 and 5, else 1" % PIPELINE_BELOW)
+                         "mode 1) and for config 2, else 1" % PIPELINE_BELOW)
     ap.add_argument("--link", type=int, default=-1, choices=[-1, 0, 1, 2, 3],
                     help="zrx_pipeline_link mode of two engines (-1: auto = 1 for configs 3/4, 0 for config 5)")
     ap.add_argument("--batches", type=int, default=2,
@@ -390,7 +390,8 @@ def bench_viterbi_only(args):
         "data": "synthetic (random bits, 802.11a encoder, soft 7*bit+U[-2,2])",
         "config": {"workload": f"config2: {n} frames x {fl} B, R=1/2, {ns} soft values each", "batches": nb},
         "bit_exact_check": {"frames_equal_sent": match, "checked": f"every frame of all {nb} batches, every engine"},
-        "pipeline": f"{len(engs)} batches in flight (engines on separate streams, steps in turn)",
+        "pipeline": (f"{len(engs)} batches in flight (engines on separate streams, steps in turn)" if len(engs) > 1
+                     else "1 batch in flight"),
         "cpu_baseline": {"value": round(done * fl * 8 / cpu_dt / 1e6, 2), "unit": "Mbit/s", "cores": threads,
                          "kind": "port", "per_core": round(done * fl * 8 / cpu_dt / 1e6 / threads, 2), "host": host,
                          "sample": f"{done} frames of the same batch, {cpu_dt:.1f} s wall on {threads} threads (CPU "
@@ -412,8 +413,11 @@ def bench_mixed(args):
           for j in range(nb)]
     gen_s = time.perf_counter() - tg
     S = max(m["max_nsym"] for m in ms)
-    # args.pipeline engines (own workspace and stream; auto: 2) take the steps in turn, as in main()
-    engs = [RxEngine(0) for _ in range(args.pipeline or 2)]
+    # args.pipeline engines (own workspace and stream; auto: 1) take the steps in turn, as in main().
+    # (Two in flight lost to one engine in interleaved A/B on one box, profiles/r04q_config5_pipeline.txt:
+    # 75.6-90.3 Gbit/s over link modes 0-2 against 93.8-94.5: the other batch's kernels take CU
+    # room from the mixed Viterbi's second block round.)
+    engs = [RxEngine(0) for _ in range(args.pipeline or 1)]
     streams = [torch.cuda.Stream(dev) for _ in engs]
     if len(engs) == 2 and args.link > 0:
         engs[0].link(engs[1], args.link)
@@ -487,7 +491,8 @@ def bench_mixed(args):
         "bit_exact_check": {"crc_pass": crc_pass, "expected_crc_pass": expect_ok, "payload_match": good,
                             "oracle_sample": sample, "oracle_sample_match": bool(oracle_match),
                             "pipeline_outputs_equal": outs_equal, "checked": f"every packet of all {nb} batches"},
-        "pipeline": f"{len(engs)} batches in flight (engines on separate streams, steps in turn)",
+        "pipeline": (f"{len(engs)} batches in flight (engines on separate streams, steps in turn)" if len(engs) > 1
+                     else "1 batch in flight"),
         "stage_ms": {k: round(v, 4) for k, v in stage.items()},
         "cpu_baseline": cpu,
     }), flush=True)

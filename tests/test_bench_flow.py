@@ -111,7 +111,7 @@ def _run(tmp_path, args):
 
 @pytest.mark.parametrize("args,k,w", [
     (["--npkts", "24", "--steps", "4", "--warmup", "2", "--no-cpu"], 4, 2),
-    (["--config", "5", "--npkts", "40", "--steps", "3", "--warmup", "1", "--cpu-seconds", "0.2"], 3, 1),
+    (["--config", "5", "--npkts", "40", "--steps", "3", "--warmup", "1", "--cpu-seconds", "0.2", "--pipeline", "2"], 3, 1),
 ])
 def test_bench_pipelined_flow(oracle, tmp_path, args, k, w):
     line, logs = _run(tmp_path, args)
