@@ -78,9 +78,9 @@ def main():
                     help="batches in flight: 2 = two engines (own workspace and stream) take the steps in "
                          "turn, as a streaming receiver would, so one batch's tail overlaps the next one's head; "
                          "0 (default) = auto: 2 for an rx batch under %d packets per GPU (zrx_pipeline_link "
-                         "mode 1) and for config 2, else 1" % PIPELINE_BELOW)
-    ap.add_argument("--link", type=int, default=-1, choices=[-1, 0, 1, 2, 3],
-                    help="zrx_pipeline_link mode of two engines (-1: auto = 1 for configs 3/4, 0 for config 5)")
+                         "mode 1) and for configs 2 and 5, else 1" % PIPELINE_BELOW)
+    ap.add_argument("--link", type=int, default=-1, choices=[-1, 0, 1, 2, 3, 4, 5, 6, 7],
+                    help="zrx_pipeline_link mode of two engines (-1: auto = 1 for configs 3/4, 4 for config 5)")
     ap.add_argument("--batches", type=int, default=2,
                     help="distinct input batches per GPU the steps rotate through (config 3/4/5)")
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 5])
@@ -413,14 +413,17 @@ def bench_mixed(args):
           for j in range(nb)]
     gen_s = time.perf_counter() - tg
     S = max(m["max_nsym"] for m in ms)
-    # args.pipeline engines (own workspace and stream; auto: 1) take the steps in turn, as in main().
-    # (Two in flight lost to one engine in interleaved A/B on one box, profiles/r04q_config5_pipeline.txt:
-    # 75.6-90.3 Gbit/s over link modes 0-2 against 93.8-94.5: the other batch's kernels take CU
-    # room from the mixed Viterbi's second block round.)
-    engs = [RxEngine(0) for _ in range(args.pipeline or 1)]
+    # args.pipeline engines (own workspace and stream; auto: 2) take the steps in turn, as in main(),
+    # linked in mode 4 by default: each batch's head (SIGNAL, plan, data FFT) on a lowest-priority
+    # stream, so the other batch's Viterbi blocks (two block rounds on a mixed batch) are dispatched
+    # first.  Interleaved on one box (profiles/r04q_config5_pipeline.txt): one engine 94.6-95.0
+    # Gbit/s, two unlinked 75.6-90.3 (the head's blocks took CU room from the Viterbi's second
+    # round), two in mode 4 101.3-101.6.
+    engs = [RxEngine(0) for _ in range(args.pipeline or 2)]
     streams = [torch.cuda.Stream(dev) for _ in engs]
-    if len(engs) == 2 and args.link > 0:
-        engs[0].link(engs[1], args.link)
+    link = 4 if args.link < 0 else args.link
+    if len(engs) == 2 and link > 0:
+        engs[0].link(engs[1], link)
     outs = []
     for e in engs:
         e.reserve(n, S)
@@ -452,6 +455,14 @@ def bench_mixed(args):
     first = k["i"]
     elapsed = _timed(step, args.steps, 0)
     timed_batches = [(first + i) % nb for i in range(args.steps)]
+    single = None
+    if len(engs) > 1:                                    # the same batches with engine 0 alone, for comparison
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for bi in timed_batches:
+            run_on(0, bi)
+        torch.cuda.synchronize()
+        single = time.perf_counter() - t0
     # every batch decoded once more by every engine: per-packet checks, engines compared
     outs_equal, good, crc_pass, expect_ok, bits_b, infos, pays = True, True, 0, 0, [], [], []
     for bi, m in enumerate(ms):
@@ -491,8 +502,9 @@ def bench_mixed(args):
         "bit_exact_check": {"crc_pass": crc_pass, "expected_crc_pass": expect_ok, "payload_match": good,
                             "oracle_sample": sample, "oracle_sample_match": bool(oracle_match),
                             "pipeline_outputs_equal": outs_equal, "checked": f"every packet of all {nb} batches"},
-        "pipeline": (f"{len(engs)} batches in flight (engines on separate streams, steps in turn)" if len(engs) > 1
-                     else "1 batch in flight"),
+        "pipeline": (f"{len(engs)} batches in flight (engines on separate streams, steps in turn, zrx_pipeline_link "
+                     f"mode {link})" if len(engs) > 1 else "1 batch in flight"),
+        "value_one_engine": round(bits * args.steps / single / 1e6, 1) if single else None,
         "stage_ms": {k: round(v, 4) for k, v in stage.items()},
         "cpu_baseline": cpu,
     }), flush=True)

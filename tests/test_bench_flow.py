@@ -129,8 +129,14 @@ def test_bench_pipelined_flow(oracle, tmp_path, args, k, w):
     warm, inst, rest = rx[:on], rx[on + 1:off], rx[off + 1:]
     assert [e[1:] for e in warm] == [[i % 2, i % nb] for i in range(w)]
     assert len(inst) >= 3 * nb and all(e[1] == 0 for e in inst) and sorted({e[2] for e in inst}) == [0, 1]
-    timed, verify = rest[:k], rest[k:k + 2 * nb]
+    timed = rest[:k]
     assert [e[1:] for e in timed] == [[(w + i) % 2, (w + i) % nb] for i in range(k)]
+    if "--config" in args:                          # config 5: engine 0 alone over the timed batches, then the checks
+        assert ["link", 0, 1, 4] in log
+        assert [e[1:] for e in rest[k:2 * k]] == [[0, (w + i) % nb] for i in range(k)]
+        assert line["value_one_engine"] > 0
+        rest = rest[k:]
+    verify = rest[k:k + 2 * nb]
     assert [e[1:] for e in verify] == [[j, bi] for bi in range(nb) for j in range(2)]
     if "--config" not in args:                      # config 3: the single-engine pass, K steps on engine 0
         assert ["link", 0, 1, 1] in log and ["plan_check", 0] in log and ["plan_check", 1] in log

@@ -414,3 +414,38 @@ def test_chain_plan_reuse(engine):
         fresh.reserve(512, S)
         assert (pay == pf).all() and (info == inf).all()
         check(x, nsym, pay, info, bad)
+
+
+@pytest.mark.parametrize("mode", [1, 2, 4, 5, 6, 7])
+def test_chain_linked_engines(mode):
+    """Two engines linked (zrx_pipeline_link bits: 1 the Viterbi waits for the peer's chain,
+    2 the data FFT waits for the peer's Viterbi, 4 the chain's head on a lowest-priority stream
+    of its own) taking mixed and uniform batches in turn on their own streams, as bench.py's
+    pipelined mode does: every output equals a lone engine's."""
+    m = txgen.make_mixed_fast(1024, min_len=64, max_len=2300, sigma=3.0, seed=81, device="cuda")
+    u = txgen.make_batch(768, seed=82, sigma=4.0, device="cuda")
+    S = max(m["max_nsym"], u["max_nsym"])
+    ref = RxEngine(0)
+    ref.reserve(1024, S)
+    exp = {}
+    for k, b in (("m", m), ("u", u)):
+        pay, info = ref.rx(b["sym"], b["sym_off"], b["nsym"], S)
+        exp[k] = (pay.cpu().numpy(), info.cpu().numpy())
+    engs = [RxEngine(0), RxEngine(0)]
+    for e in engs:
+        e.reserve(1024, S)
+    engs[0].link(engs[1], mode)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for st in streams:
+        st.wait_stream(torch.cuda.current_stream())
+    outs = []
+    for i, k in enumerate("mumummuu"):
+        b = m if k == "m" else u
+        with torch.cuda.stream(streams[i % 2]):
+            pay, info = engs[i % 2].rx(b["sym"], b["sym_off"], b["nsym"], S)
+        outs.append((k, pay, info))
+    torch.cuda.synchronize()
+    for k, pay, info in outs:
+        assert (pay.cpu().numpy() == exp[k][0]).all() and (info.cpu().numpy() == exp[k][1]).all(), k
+    assert (exp["u"][1][:, 4] == 1).all()
+    engs[0].link(engs[1], 0)

@@ -98,6 +98,10 @@ struct zrx_ctx {
   zrx_ctx* peer = nullptr;
   int link_mode = 0;
   hipEvent_t ev_vit_done = nullptr, ev_chain_done = nullptr;   // recorded every chain while linked
+  // link mode 4: the chain's head (SIGNAL .. k_data_fft) on a low-priority stream of its own,
+  // forked from and joined back into the caller's stream
+  hipStream_t lo = nullptr;
+  hipEvent_t ev_lo_fork = nullptr, ev_lo_join = nullptr;
 };
 
 static int check_device(int device) {
@@ -456,6 +460,11 @@ int zrx_destroy(zrx_ctx* c) {
   if (c->peer) { c->peer->peer = nullptr; c->peer->link_mode = 0; }
   if (c->ev_vit_done) (void)hipEventDestroy(c->ev_vit_done);
   if (c->ev_chain_done) (void)hipEventDestroy(c->ev_chain_done);
+  if (c->lo) {
+    (void)hipStreamDestroy(c->lo);
+    (void)hipEventDestroy(c->ev_lo_fork);
+    (void)hipEventDestroy(c->ev_lo_join);
+  }
   if (c->side) {
     (void)hipStreamDestroy(c->side);
     (void)hipEventDestroy(c->ev_fork);
@@ -472,7 +481,7 @@ int zrx_set_stream(zrx_ctx* c, void* stream) {
 }
 
 int zrx_pipeline_link(zrx_ctx* a, zrx_ctx* b, int mode) {
-  if (!a || !b || a == b || mode < 0 || mode > 3) return ZRX_EINVAL;
+  if (!a || !b || a == b || mode < 0 || mode > 7) return ZRX_EINVAL;
   for (zrx_ctx* c : {a, b}) {
     if (c->peer && c->peer != a && c->peer != b) { c->peer->peer = nullptr; c->peer->link_mode = 0; }
     // stream-to-stream on one device: no system-scope fence (which writes back the L2s)
@@ -480,6 +489,13 @@ int zrx_pipeline_link(zrx_ctx* a, zrx_ctx* b, int mode) {
       ZRX_CHECK(hipEventCreateWithFlags(&c->ev_vit_done, hipEventDisableTiming | hipEventDisableSystemFence));
     if (!c->ev_chain_done)
       ZRX_CHECK(hipEventCreateWithFlags(&c->ev_chain_done, hipEventDisableTiming | hipEventDisableSystemFence));
+    if ((mode & 4) && !c->lo) {
+      int least = 0, greatest = 0;
+      ZRX_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      ZRX_CHECK(hipStreamCreateWithPriority(&c->lo, hipStreamNonBlocking, least));
+      ZRX_CHECK(hipEventCreateWithFlags(&c->ev_lo_fork, hipEventDisableTiming | hipEventDisableSystemFence));
+      ZRX_CHECK(hipEventCreateWithFlags(&c->ev_lo_join, hipEventDisableTiming | hipEventDisableSystemFence));
+    }
   }
   a->peer = mode ? b : nullptr;
   b->peer = mode ? a : nullptr;
@@ -640,6 +656,16 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
   }
   const uint32_t* chan = (const uint32_t*)d_chan;
   hipStream_t s = c->stream;
+  // h: the stream of the chain's head (SIGNAL, plan, k_data_fft): the caller's, or with link
+  // mode 4 a low-priority stream of the context, so that where two linked engines overlap the
+  // other batch's Viterbi blocks are dispatched before this batch's head blocks.
+  const bool lo = c->peer && (c->link_mode & 4) && c->lo;
+  hipStream_t h = s;
+  if (lo) {
+    ZRX_CHECK(hipEventRecord(c->ev_lo_fork, s));
+    ZRX_CHECK(hipStreamWaitEvent(c->lo, c->ev_lo_fork, 0));
+    h = c->lo;
+  }
   hipEvent_t* ev = nullptr;
   if (c->timing) {
     if (c->nrec == c->evsets.size()) {
@@ -649,19 +675,19 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
     }
     ev = c->evsets[c->nrec++].data();
   }
-  if (ev) ZRX_CHECK(hipEventRecord(ev[0], s));
+  if (ev) ZRX_CHECK(hipEventRecord(ev[0], h));
   // one lane per packet, kSigFftLanes packets per one-wave block.  (16 measured worse: 9.4 ->
   // 14.3 us at config 3, and with two engines in flight its 1024 single-wave blocks took CU
   // slots the other batch's Viterbi blocks were placed by: config 5 101 -> 76 Gbit/s.)
   if (chan)
-    k_signal_fft<true><<<blocks(npkts, kSigFftLanes), kSigFftLanes, 0, s>>>((const uint4*)d_sym, d_sym_off, d_nsym,
+    k_signal_fft<true><<<blocks(npkts, kSigFftLanes), kSigFftLanes, 0, h>>>((const uint4*)d_sym, d_sym_off, d_nsym,
                                                                             npkts, (uint4*)c->sig_soft, chan, T);
   else
-    k_signal_fft<false><<<blocks(npkts, kSigFftLanes), kSigFftLanes, 0, s>>>((const uint4*)d_sym, d_sym_off, d_nsym,
+    k_signal_fft<false><<<blocks(npkts, kSigFftLanes), kSigFftLanes, 0, h>>>((const uint4*)d_sym, d_sym_off, d_nsym,
                                                                              npkts, (uint4*)c->sig_soft, chan, T);
-  if (ev) ZRX_CHECK(hipEventRecord(ev[1], s));
+  if (ev) ZRX_CHECK(hipEventRecord(ev[1], h));
   const bool ordered = order_fits(c, npkts);
-  k_signal_vit<<<blocks(npkts, v3::kRows), 256, 0, s>>>(c->sig_soft, d_nsym, npkts, c->cap_nsym, c->vparams, d_info,
+  k_signal_vit<<<blocks(npkts, v3::kRows), 256, 0, h>>>(c->sig_soft, d_nsym, npkts, c->cap_nsym, c->vparams, d_info,
                                                  ordered ? c->nrows : nullptr);
   // A mixed batch's sort and row expansion (k_pkt_rows) only feed the Viterbi, so they can run
   // on a side stream while k_data_fft runs (config 5: -27 us a batch).  The fork and join cost
@@ -676,7 +702,7 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
     *(volatile int32_t*)c->mixed_hint = 0;
   }
   const bool split = ordered && *(volatile int32_t*)c->mixed_hint != 0;
-  k_pkt_plan<<<1, 1024, 0, s>>>(c->vparams, npkts, c->soft_off, c->dsym, c->wave_p0, ordered ? c->rows : nullptr,
+  k_pkt_plan<<<1, 1024, 0, h>>>(c->vparams, npkts, c->soft_off, c->dsym, c->wave_p0, ordered ? c->rows : nullptr,
                                 c->nrows, c->segs, c->order, c->dec_bits, c->ncu, (int)plan_rows_max(c, npkts),
                                 split ? 1 : 0, ordered ? c->mixed_hint_dev : nullptr);
   if (split) {
@@ -686,29 +712,33 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
       ZRX_CHECK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming | hipEventDisableSystemFence));
       ZRX_CHECK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming | hipEventDisableSystemFence));
     }
-    ZRX_CHECK(hipEventRecord(c->ev_fork, s));
+    ZRX_CHECK(hipEventRecord(c->ev_fork, h));
     ZRX_CHECK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
     k_pkt_rows<<<1, 1024, 0, c->side>>>(c->vparams, npkts, c->rows, c->nrows, c->segs, c->order, c->dec_bits, c->ncu,
                                         (int)plan_rows_max(c, npkts));
     ZRX_CHECK(hipEventRecord(c->ev_join, c->side));
   }
-  if (ev) ZRX_CHECK(hipEventRecord(ev[2], s));
+  if (ev) ZRX_CHECK(hipEventRecord(ev[2], h));
   // k_data_fft: waves over the batch's data symbols, at most npkts x (max_nsym - 1) of them
   const int fft_blocks = (int)std::min<int64_t>(((int64_t)npkts * (max_nsym - 1) + 255) / 256,
                                                 (int64_t)(chan ? c->df_blocks_eq : c->df_blocks));
   zrx_ctx* const peer = c->peer;
   // (a never-recorded peer event is complete: the first batch waits for nothing)
-  if (peer && (c->link_mode & 2)) ZRX_CHECK(hipStreamWaitEvent(s, peer->ev_vit_done, 0));
+  if (peer && (c->link_mode & 2)) ZRX_CHECK(hipStreamWaitEvent(h, peer->ev_vit_done, 0));
   if (fft_blocks > 0) {
     if (chan)
-      k_data_fft<true><<<fft_blocks, 256, 0, s>>>((const uint4*)d_sym, d_sym_off, c->vparams, npkts, (uint4*)c->soft,
+      k_data_fft<true><<<fft_blocks, 256, 0, h>>>((const uint4*)d_sym, d_sym_off, c->vparams, npkts, (uint4*)c->soft,
                                                    c->soft_off, c->dsym, c->wave_p0, chan, T);
     else
-      k_data_fft<false><<<fft_blocks, 256, 0, s>>>((const uint4*)d_sym, d_sym_off, c->vparams, npkts, (uint4*)c->soft,
+      k_data_fft<false><<<fft_blocks, 256, 0, h>>>((const uint4*)d_sym, d_sym_off, c->vparams, npkts, (uint4*)c->soft,
                                                     c->soft_off, c->dsym, c->wave_p0, chan, T);
   }
-  if (ev) ZRX_CHECK(hipEventRecord(ev[3], s));
+  if (ev) ZRX_CHECK(hipEventRecord(ev[3], h));
   if (split) ZRX_CHECK(hipStreamWaitEvent(s, c->ev_join, 0));
+  if (lo) {
+    ZRX_CHECK(hipEventRecord(c->ev_lo_join, h));
+    ZRX_CHECK(hipStreamWaitEvent(s, c->ev_lo_join, 0));
+  }
   if (peer && (c->link_mode & 1)) ZRX_CHECK(hipStreamWaitEvent(s, peer->ev_chain_done, 0));
   launch_viterbi(c, c->soft, c->soft_off, c->vparams, npkts, c->dec, c->dec_off, c->dec_bits, ordered);
   if (peer) ZRX_CHECK(hipEventRecord(c->ev_vit_done, s));

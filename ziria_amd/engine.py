@@ -70,7 +70,8 @@ class RxEngine:
     def link(self, other, mode):
         """Two engines taking a stream of batches in turn (zrx_pipeline_link): mode bit 0 =
         this engine's data Viterbi waits for the other's last launched chain, bit 1 = its data
-        FFT waits for the other's last launched Viterbi; 0 unlinks."""
+        FFT waits for the other's last launched Viterbi, bit 2 = its chain's head (SIGNAL,
+        plan, data FFT) on a lowest-priority stream; 0 unlinks."""
         check(lib().zrx_pipeline_link(self._h, other._h, int(mode)), "zrx_pipeline_link")
 
     # ------------------------------------------------------------------ launches
