@@ -138,6 +138,19 @@ def crc_shift_n_tables(mats, unit_bytes):
     return out
 
 
+def crc_ones_shift(n_max=2048):
+    """A^n(0xFFFFFFFF), n < n_max: the register an all-ones initial value becomes after n
+    zero bytes.  By linearity the reference's CRC (all-ones init, crc.blk:85-118) of n bytes
+    is ~(U0(data) ^ A^n(~0)) with U0 the zero-initialised register, so k_descramble_crc runs
+    the zero-initialised CRC on the payload as it is and corrects with one table word."""
+    T = crc_table()
+    out, r = [], 0xFFFFFFFF
+    for _ in range(n_max):
+        out.append(r)
+        r = T[r & 0xFF] ^ (r >> 8)
+    return out
+
+
 def crc_slice4():
     """Slicing-by-4 tables: S[0] = the byte table, S[k][b] = S[k-1][b] after one zero byte."""
     T = crc_table()
@@ -212,6 +225,8 @@ def render():
     L.append("static constexpr uint32_t kCrcShift[6][128] = {" + ", ".join(
         "{" + ", ".join(f"0x{v:08x}u" for v in T[k * 128:(k + 1) * 128]) + "}" for k in range(6)) + "};")
     S4 = crc_slice4()
+    L.append("// kCrcOnes[n]: the all-ones CRC register after n zero bytes (crc_ones_shift)")
+    L.append("static constexpr uint32_t kCrcOnes[2048] = {" + ", ".join(f"0x{v:08x}u" for v in crc_ones_shift()) + "};")
     L.append("// slicing-by-4 CRC tables: kCrcS4[k][b] = byte table entry advanced by k zero bytes")
     L.append("static constexpr uint32_t kCrcS4[4][256] = {" + ", ".join(
         "{" + ", ".join(f"0x{v:08x}u" for v in S) + "}" for S in S4) + "};")

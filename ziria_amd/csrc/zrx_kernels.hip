@@ -744,26 +744,34 @@ __global__ __launch_bounds__(256) void k_ofdm_eq(const uint4* __restrict__ sym, 
 
 // ------------------------------------------------------------------ descramble + CRC
 // info[8p+4] = crc_ok, info[8p+7] = viterbi bits; payload gets len-4 descrambled bytes.
-// One wave per packet, kCrcWaves packets per block.
+// One wave per packet, kCrcWaves packets per block.  The kernel is VALU-bound (8 waves a SIMD,
+// ≈ 500 instructions a packet before this form), so the work per packet is what counts:
 //  * Descrambler (Decode.blk:36-43, scramble.blk:28-44): the keystream of SERVICE state S is
 //    one 127-periodic byte sequence read from phase 16*phase(S), so the payload is written
-//    with coalesced dword stores (256 B per store instruction).
-//  * CRC-32 check (crc.blk:85-118, = zlib): the zero-initialised CRC of the payload with its
-//    first 4 bytes complemented equals the reference's all-ones-initialised one; leading
-//    zero bytes leave a zero register unchanged, so the payload is right-aligned in a
-//    2048-byte frame and lane L takes bytes [32L, 32L+32) as 8 dwords (slicing-by-4).  Each
+//    with coalesced dword stores (256 B per store instruction).  Dword i = decoded bytes
+//    2+4i .. 5+4i: the upper neighbour word comes from lane + 1 by a wave_shl DPP move, the
+//    keystream word from a doubled table at a per-lane base (no wrap test), bytes past the
+//    payload are masked (one 64-bit shift, in the iterations that reach the payload's end).  The masked words also go to the wave's
+//    LDS region, behind 8 zero words.
+//  * CRC-32 check (crc.blk:85-118, = zlib): by linearity the reference's all-ones-initialised
+//    register is the zero-initialised one XOR kCrcOnes[n] (the all-ones value after n zero
+//    bytes), and leading zero bytes leave a zero register unchanged, so the payload is
+//    right-aligned in a 2048-byte frame and lane L takes bytes [32L, 32L+32) (slicing-by-4)
+//    straight from the LDS copy — zeros before the payload, no keystream, no masks.  Each
 //    lane's register is advanced past the 32*(63-L) bytes behind its chunk with two
 //    nibble-sliced zero-byte tables of its own (((63-L) & 7) x 32 and ((63-L) >> 3) x 256
-//    bytes: 16 lookups, not one table per bit of 63-L) and the wave XORs the 64 registers.
+//    bytes: 16 lookups) and the wave XORs the 64 registers.
 constexpr int kCrcWaves = 8;
+constexpr int kCrcGuard = 8;                          // zero words before a wave's payload copy
 __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t* __restrict__ dec,
                                                                    const int32_t* __restrict__ dec_bits,
                                                                    int32_t* __restrict__ info, uint8_t* __restrict__ payload,
                                                                    int npkts) {
   __shared__ uint32_t s4[4][256];
   __shared__ uint32_t shf[16][128];                   // [n]: n * 32 zero bytes, [8 + n]: n * 256
-  __shared__ uint32_t scrw[128];
+  __shared__ uint32_t scrw2[256];                     // keystream words, doubled: [n] = kScrW[n mod 127]
   __shared__ uint8_t scrb[256];
+  __shared__ uint32_t pw_all[kCrcWaves][kCrcGuard + 512];   // per wave: zero guard, payload dwords
   {                                                    // every table load in flight at once
     static_assert(64 * kCrcWaves == 512, "two words of each 1024-word table per thread");
     const int t = threadIdx.x;
@@ -771,17 +779,18 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
     const uint32_t* SL = &kCrcShiftLo[0][0];
     const uint32_t* SH = &kCrcShiftHi[0][0];
     const uint32_t a0 = S4[t], a1 = S4[t + 512], b0 = SL[t], b1 = SL[t + 512], c0 = SH[t], c1 = SH[t + 512];
-    const uint32_t d = kScrW[min(t, 126)];
+    const uint32_t d2 = kScrW[t < 127 ? t : t < 254 ? t - 127 : 0];
     const uint8_t e = kScrB2[min(t, 253)];
     (&s4[0][0])[t] = a0; (&s4[0][0])[t + 512] = a1;
     (&shf[0][0])[t] = b0; (&shf[0][0])[t + 512] = b1;
     (&shf[8][0])[t] = c0; (&shf[8][0])[t + 512] = c1;
-    if (t < 127) scrw[t] = d;
-    if (t < 254) scrb[t] = e;
+    if (t < 254) { scrw2[t] = d2; scrb[t] = e; }
+    if ((t & 63) < kCrcGuard) pw_all[t >> 6][t & 63] = 0u;
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // (packet values below: scalar)
+  uint32_t* pw = pw_all[wv] + kCrcGuard;              // payload dword i at pw[i]; pw[-8 .. -1] = 0
   // grid-stride over packets (one wave per packet at a time): the LDS tables above are
   // staged once per block, not once per 8 packets.  Decoded bytes are read and payload
   // dwords written by buffer ops on the packet's own slot: 32-bit lane offsets, and a word
@@ -797,6 +806,10 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
     }
     const uint8_t* d = dec + (int64_t)p * kDecStride;
     const int plen = len - 4;
+    // the received CRC: decoded bytes 2 + plen .. 5 + plen (scalar loads, used at the end)
+    const uint32_t* dw = (const uint32_t*)d;
+    const int tb = (2 + plen) >> 2;
+    const uint32_t t0 = dw[tb], t1 = dw[tb + 1];
     const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)d, (short)0, kDecStride, 0x00020000);
     const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)(payload + (int64_t)p * kPayloadStride),
                                                                          (short)0, (plen + 3) & ~3, 0x00020000);
@@ -805,55 +818,36 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
     const int n0 = (16 * (int)kScrPhase[S]) % 127;
     // payload: dword i = decoded bytes 2+4i .. 5+4i.  The lane's dwords i = lane + 64k
     // (k < 8: plen <= 2044) are all loaded before any is used (one memory latency per packet,
-    // not one per iteration); the upper neighbour word comes from lane + 1.
+    // not one per iteration).
     uint32_t wv9[9];
 #pragma unroll
     for (int k = 0; k < 9; k++) wv9[k] = __builtin_amdgcn_raw_buffer_load_b32(rd, 4 * (lane + 64 * k), 0, 0);
-    int n = (n0 + 4 * lane) % 127;
+    const uint32_t* ks = scrw2 + (n0 + 4 * lane) % 127;   // keystream word of dword lane + 64k: ks[2k]
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       const int i = lane + 64 * k;
-      const uint32_t dn = (uint32_t)__shfl_down((int)wv9[k], 1);
-      const uint32_t nx = lane == 63 ? (uint32_t)__builtin_amdgcn_readlane((int)wv9[k + 1], 0) : dn;
-      uint32_t v = __builtin_amdgcn_alignbyte(nx, wv9[k], 2) ^ (scrw[n] & ksm);
-      const int rem = plen - 4 * i;                    // (a dword at or past the payload end: dropped)
-      if (rem < 4) v &= rem > 0 ? 0xFFFFFFFFu >> (32 - 8 * rem) : 0u;
-      __builtin_amdgcn_raw_buffer_store_b32(v, rp, 4 * i, 0, 0);
-      n += 2;                                          // 256 bytes on: 256 = 2 mod 127
-      if (n >= 127) n -= 127;
+      // dword i + 1: lane + 1's word k (wave_shl:1), lane 63's from lane 0's word k + 1
+      const uint32_t up = (uint32_t)__builtin_amdgcn_readfirstlane((int)wv9[k + 1]);
+      const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp((int)up, (int)wv9[k], 0x130, 0xF, 0xF, false);
+      uint32_t v = __builtin_amdgcn_alignbyte(nx, wv9[k], 2) ^ (ks[2 * k] & ksm);
+      if (4 * (64 * k + 64) > plen)                    // (wave-uniform) bytes past the payload := 0
+        v &= (uint32_t)(0xFFFFFFFFull >> (32 - 8 * min(max(plen - 4 * i, 0), 4)));
+      __builtin_amdgcn_raw_buffer_store_b32(v, rp, 4 * i, 0, 0);   // (past the payload: dropped)
+      pw[i] = v;
     }
+    __builtin_amdgcn_wave_barrier();
     uint32_t crc;
     if (plen >= 4) {
       const int q0 = 32 * lane - (2048 - plen);        // payload index of this lane's first byte
-      // (a chunk wholly before the payload: every word masked to 0 below, so r stays 0)
-      const int g = 2 + q0;                            // decoded-byte index of the first byte
-      const int a = g >> 2;                            // (arithmetic: negative before the slot)
-      const int sh = g & 3;
+      const int a = q0 >> 2;                           // (arithmetic: negative before the payload)
+      const int sh = q0 & 3;
       uint32_t w[9];
 #pragma unroll
-      for (int j = 0; j < 9; j++) w[j] = __builtin_amdgcn_raw_buffer_load_b32(rd, 4 * max(a + j, 0), 0, 0);
-      int m = (n0 + q0 + 127 * 17) % 127;              // (q0 > -2048 = -127 x 17 + 111)
-      uint32_t x[8];
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        x[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh) ^ (scrw[m] & ksm);
-        m += 4;
-        if (m >= 127) m -= 127;
-      }
-      if (q0 < 4) {                                    // chunk holds the payload start (or lies before it)
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-          const int qf = q0 + 4 * j;                   // payload index of byte 0 of word j
-          if (qf <= -4) x[j] = 0;
-          else if (qf < 0) x[j] &= 0xFFFFFFFFu << (-8 * qf);   // bytes before the payload
-          if (qf > -4 && qf < 4)                                // complement payload bytes 0..3
-            x[j] ^= qf >= 0 ? 0xFFFFFFFFu >> (8 * qf) : 0xFFFFFFFFu << (-8 * qf);
-        }
-      }
+      for (int j = 0; j < 9; j++) w[j] = pw[max(a + j, -kCrcGuard)];   // (before the payload: zeros)
       uint32_t r = 0;
 #pragma unroll
       for (int j = 0; j < 8; j++) {
-        r ^= x[j];
+        r ^= __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
         r = s4[3][r & 0xFFu] ^ s4[2][(r >> 8) & 0xFFu] ^ s4[1][(r >> 16) & 0xFFu] ^ s4[0][r >> 24];
       }
       // advance past the 63 - lane 32-byte chunks behind this one: (63 - lane) & 7 chunks,
@@ -861,13 +855,13 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
       const uint32_t adv = 63u - (uint32_t)lane;
 #pragma unroll
       for (int k = 0; k < 2; k++) {
-        const uint32_t* tb = shf[k ? 8u + (adv >> 3) : (adv & 7u)];
+        const uint32_t* tb2 = shf[k ? 8u + (adv >> 3) : (adv & 7u)];
         uint32_t t = 0;
 #pragma unroll
-        for (int j = 0; j < 8; j++) t ^= tb[j * 16 + ((r >> (4 * j)) & 15u)];
+        for (int j = 0; j < 8; j++) t ^= tb2[j * 16 + ((r >> (4 * j)) & 15u)];
         r = t;
       }
-      crc = ~wave_xor_u32(r);
+      crc = ~(wave_xor_u32(r) ^ kCrcOnes[plen]);
     } else {                                           // < 4 payload bytes: the plain register
       crc = 0xFFFFFFFFu;
       for (int q = 0; q < plen; q++)
@@ -875,11 +869,10 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
       crc = ~crc;
     }
     if (lane == 0) {
-      uint32_t rx = 0;
-      const int m = (n0 + plen) % 127;
-      for (int k = 0; k < 4; k++) rx |= ((uint32_t)d[2 + plen + k] ^ (scrb[m + k] & ksm)) << (8 * k);
+      const uint32_t rx = __builtin_amdgcn_alignbyte(t1, t0, (2 + plen) & 3) ^ (scrw2[(n0 + plen) % 127] & ksm);
       in[4] = crc == rx ? 1 : 0;
     }
+    __builtin_amdgcn_wave_barrier();                   // (this packet's LDS reads before the next one's writes)
   }
 }
 
