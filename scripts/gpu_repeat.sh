@@ -1,6 +1,6 @@
 #!/bin/bash
-# descramble/CRC with fewer instructions per packet (CRC from the LDS payload copy, all-ones
-# init by table, wave_shl neighbour words) against the previous commit (prev).
+# descramble/CRC with the slot loads issued with the header loads and the scrambler state
+# from the slot's first word (one dependent load less) against the previous commit (prev).
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }

@@ -771,6 +771,7 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
   __shared__ uint32_t shf[16][128];                   // [n]: n * 32 zero bytes, [8 + n]: n * 256
   __shared__ uint32_t scrw2[256];                     // keystream words, doubled: [n] = kScrW[n mod 127]
   __shared__ uint8_t scrb[256];
+  __shared__ uint8_t scrph[128];
   __shared__ uint32_t pw_all[kCrcWaves][kCrcGuard + 512];   // per wave: zero guard, payload dwords
   {                                                    // every table load in flight at once
     static_assert(64 * kCrcWaves == 512, "two words of each 1024-word table per thread");
@@ -780,11 +781,12 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
     const uint32_t* SH = &kCrcShiftHi[0][0];
     const uint32_t a0 = S4[t], a1 = S4[t + 512], b0 = SL[t], b1 = SL[t + 512], c0 = SH[t], c1 = SH[t + 512];
     const uint32_t d2 = kScrW[t < 127 ? t : t < 254 ? t - 127 : 0];
-    const uint8_t e = kScrB2[min(t, 253)];
+    const uint8_t e = kScrB2[min(t, 253)], f = kScrPhase[t & 127];
     (&s4[0][0])[t] = a0; (&s4[0][0])[t + 512] = a1;
     (&shf[0][0])[t] = b0; (&shf[0][0])[t + 512] = b1;
     (&shf[8][0])[t] = c0; (&shf[8][0])[t + 512] = c1;
     if (t < 254) { scrw2[t] = d2; scrb[t] = e; }
+    if (t < 128) scrph[t] = f;
     if ((t & 63) < kCrcGuard) pw_all[t >> 6][t & 63] = 0u;
   }
   __syncthreads();
@@ -797,6 +799,14 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
   // outside the slot (load: 0) or past the payload (store: dropped) needs no branch.
   for (int p = blockIdx.x * kCrcWaves + wv; p < npkts; p += gridDim.x * kCrcWaves) {
     int32_t* in = info + 8 * (int64_t)p;
+    const uint8_t* d = dec + (int64_t)p * kDecStride;
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)d, (short)0, kDecStride, 0x00020000);
+    // payload: dword i = decoded bytes 2+4i .. 5+4i.  The lane's dwords i = lane + 64k
+    // (k < 8: plen <= 2044) are loaded with the header fields, before any of them is looked at
+    // (a packet that turns out to have no payload wastes them).
+    uint32_t wv9[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) wv9[k] = __builtin_amdgcn_raw_buffer_load_b32(rd, 4 * (lane + 64 * k), 0, 0);
     const int len = in[2], status = in[5];
     const int bits = dec_bits[p];
     if (lane == 0) in[7] = bits;
@@ -804,24 +814,17 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
       if (lane == 0) in[4] = 0;
       continue;
     }
-    const uint8_t* d = dec + (int64_t)p * kDecStride;
     const int plen = len - 4;
     // the received CRC: decoded bytes 2 + plen .. 5 + plen (scalar loads, used at the end)
     const uint32_t* dw = (const uint32_t*)d;
     const int tb = (2 + plen) >> 2;
     const uint32_t t0 = dw[tb], t1 = dw[tb + 1];
-    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)d, (short)0, kDecStride, 0x00020000);
     const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)(payload + (int64_t)p * kPayloadStride),
                                                                          (short)0, (plen + 3) & ~3, 0x00020000);
-    const uint32_t S = (uint32_t)d[1] >> 1;           // SERVICE bits 9..15 = scrambler state
+    // SERVICE bits 9..15 = scrambler state (decoded byte 1: lane 0's first word)
+    const uint32_t S = ((uint32_t)__builtin_amdgcn_readfirstlane((int)wv9[0]) >> 9) & 0x7Fu;
     const uint32_t ksm = S == 0 ? 0u : 0xFFFFFFFFu;   // state 0 never leaves 0: zero keystream
-    const int n0 = (16 * (int)kScrPhase[S]) % 127;
-    // payload: dword i = decoded bytes 2+4i .. 5+4i.  The lane's dwords i = lane + 64k
-    // (k < 8: plen <= 2044) are all loaded before any is used (one memory latency per packet,
-    // not one per iteration).
-    uint32_t wv9[9];
-#pragma unroll
-    for (int k = 0; k < 9; k++) wv9[k] = __builtin_amdgcn_raw_buffer_load_b32(rd, 4 * (lane + 64 * k), 0, 0);
+    const int n0 = (16 * (int)scrph[S]) % 127;
     const uint32_t* ks = scrw2 + (n0 + 4 * lane) % 127;   // keystream word of dword lane + 64k: ks[2k]
 #pragma unroll
     for (int k = 0; k < 8; k++) {
