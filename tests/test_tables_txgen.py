@@ -72,6 +72,21 @@ def test_crc_tables():
         assert apply(Z[k], v) == w
 
 
+def test_crc_ones_identity():
+    """k_descramble_crc's form of the reference CRC (all-ones init, crc.blk:85-118 = zlib):
+    the zero-initialised register of the payload XOR kCrcOnes[n], complemented, for payloads
+    of every length class the kernel sees (its < 4-byte path aside)."""
+    a = _header_arrays()
+    tab, ones = a["kCrcTab"], a["kCrcOnes"]
+    rng = np.random.default_rng(5)
+    for n in (4, 5, 31, 32, 33, 255, 1500, 2043, 2044):
+        data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        reg = 0
+        for b in data:
+            reg = int(tab[(reg ^ b) & 0xFF]) ^ (reg >> 8)
+        assert (~(reg ^ int(ones[n]))) & 0xFFFFFFFF == zlib.crc32(data), n
+
+
 def test_scrambler_tables():
     a = _header_arrays()
     phase, kb = a["kScrPhase"], a["kScrByte"]
