@@ -1,11 +1,6 @@
 #!/bin/bash
-# HIP stream priority range on this box.
+# GPU parity suite (with the scrambler-state / short-payload chain test).
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-timeout -k 10 120 python -c "
-import torch
-print('torch priority_range', torch.cuda.Stream.priority_range())
-import ctypes
-h = ctypes.CDLL('libamdhip64.so')
-lo, hi = ctypes.c_int(), ctypes.c_int()
-print('hip', h.hipDeviceGetStreamPriorityRange(ctypes.byref(lo), ctypes.byref(hi)), lo.value, hi.value)
-"
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -1 gpurun_out/pytest_gpu.log

@@ -449,3 +449,26 @@ def test_chain_linked_engines(mode):
         assert (pay.cpu().numpy() == exp[k][0]).all() and (info.cpu().numpy() == exp[k][1]).all(), k
     assert (exp["u"][1][:, 4] == 1).all()
     engs[0].link(engs[1], 0)
+
+
+def test_chain_scrambler_states_and_short_payloads(engine, oracle):
+    """The descrambler and CRC (k_descramble_crc) across scrambler states — every keystream
+    phase the SERVICE field can announce, the stuck state 0 among them — and payload lengths
+    around the kernel's boundaries (0..5 bytes: the plain-register path; 31..33, 255..257:
+    chunk and dword edges; 2044: the largest): payloads and infos equal the oracle receiver's
+    and, every CRC passing, the transmitted payloads."""
+    states = np.arange(128) % 128
+    for L, (mod, cod) in ((0, (0, 0)), (1, (1, 2)), (2, (3, 2)), (3, (2, 0)), (4, (3, 1)), (5, (0, 2)),
+                          (31, (3, 2)), (32, (2, 2)), (33, (1, 0)), (255, (3, 2)), (256, (3, 1)), (257, (2, 0)),
+                          (2044, (3, 2))):
+        n = 128
+        b = txgen.make_batch(n, mod=mod, coding=cod, payload_len=L, sigma=2.0, seed=300 + L, device="cuda",
+                             scrambler=np.roll(states, L))
+        engine.reserve(n, b["max_nsym"])
+        pay, info = engine.rx(b["sym"], b["sym_off"], b["nsym"], b["max_nsym"])
+        pay, info = pay.cpu().numpy(), info.cpu().numpy()
+        sym = b["sym"].cpu().numpy()
+        opay, res = oracle.rx_batch_time(sym, b["sym_off"].cpu().numpy(), b["nsym"].cpu().numpy())
+        for i, r in enumerate(res):
+            assert info[i, 2] == r["len"] == L + 4 and info[i, 4] == r["crc_ok"] == 1, (L, i)
+            assert (pay[i, :L] == opay[i, :L]).all() and (pay[i, :L] == b["payload"][i]).all(), (L, i)

@@ -41,8 +41,10 @@ def interleave_perm(mod):
     return s * (i // s) + (i + N - (16 * i) // N) % s
 
 
-def _scrambler_keystream(n):
-    st = [1, 0, 1, 1, 1, 0, 1]                       # default_scrmbl_st (scramble.blk:22)
+def _scrambler_keystream(n, state=None):
+    """Keystream bits of the x^7+x^4+1 scrambler (scramble.blk:28-44) from a 7-bit initial
+    state (bit k = st[k]); default default_scrmbl_st = 1011101 (scramble.blk:22)."""
+    st = [1, 0, 1, 1, 1, 0, 1] if state is None else [(int(state) >> k) & 1 for k in range(7)]
     out = np.zeros(n, np.uint8)
     for k in range(n):
         t = st[3] ^ st[0]
@@ -95,9 +97,10 @@ def _signal_levels(mod, coding, length, device):
     return re * UNIT[0]
 
 
-def packets_freq(payloads, mod, coding, device="cpu"):
+def packets_freq(payloads, mod, coding, device="cpu", scrambler=None):
     """Frequency-domain symbols (GetData order, TX units) for equal-length payloads.
-    payloads: uint8 numpy [n, L].  Returns int64 torch [n, 1 + nsym, 48, 2]."""
+    payloads: uint8 numpy [n, L]; scrambler: None (the default state for every packet) or
+    one 7-bit initial scrambler state per packet.  Returns int64 torch [n, 1 + nsym, 48, 2]."""
     n, L = payloads.shape
     nd, nc = ndbps(mod, coding), NCBPS[mod]
     nsym = n_data_symbols(mod, coding, L)
@@ -106,7 +109,11 @@ def packets_freq(payloads, mod, coding, device="cpu"):
     bits[:, 16:16 + 8 * L] = np.unpackbits(payloads, axis=1, bitorder="little")
     crc = np.array([zlib.crc32(p.tobytes()) for p in payloads], np.uint32)
     bits[:, 16 + 8 * L:16 + 8 * L + 32] = ((crc[:, None] >> np.arange(32, dtype=np.uint32)) & 1).astype(np.uint8)
-    bits ^= _scrambler_keystream(nbits)[None]
+    if scrambler is None:
+        bits ^= _scrambler_keystream(nbits)[None]
+    else:
+        ks = {int(v): _scrambler_keystream(nbits, v) for v in np.unique(scrambler)}
+        bits ^= np.stack([ks[int(v)] for v in scrambler])
     u = torch.from_numpy(bits).to(device)
     coded = _encode(u, coding).reshape(n, nsym, nc)
     perm = torch.from_numpy(interleave_perm(mod)).to(device)
@@ -175,17 +182,19 @@ def to_time(freq, sigma, gen, atten=100.0, channel=False):
 
 
 def make_batch(n, mod=3, coding=2, payload_len=1500, sigma=4.0, seed=0x5EED, device="cpu", chunk=2048,
-               channel=False):
+               channel=False, scrambler=None):
     """BASELINE config 3 shape by default: n packets of payload_len bytes at (mod, coding).
     Returns dict(sym int16 [n*S,64,2], sym_off int64 [n], nsym int32 [n], payload uint8
-    [n, L], max_nsym); channel=True adds the channel of to_time and chan int16 [n,64,2]."""
+    [n, L], max_nsym); channel=True adds the channel of to_time and chan int16 [n,64,2];
+    scrambler: per-packet initial scrambler states (packets_freq), default the reference's."""
     rng = np.random.default_rng(seed)
     gen = torch.Generator(device=device)
     gen.manual_seed(seed)
     payloads = rng.integers(0, 256, (n, payload_len), dtype=np.uint8)
     syms, chans = [], []
     for a in range(0, n, chunk):
-        f = packets_freq(payloads[a:a + chunk], mod, coding, device)
+        f = packets_freq(payloads[a:a + chunk], mod, coding, device,
+                         scrambler=None if scrambler is None else np.asarray(scrambler)[a:a + chunk])
         t = to_time(f, sigma, gen, channel=channel)
         if channel:
             t, c = t
