@@ -1,5 +1,5 @@
 #!/bin/bash
-# k_signal_fft with the symbol loads ahead of the LUT staging (no barrier: one-wave blocks)
+# descramble/CRC loading the next packet's slot and header while working on this one
 # against the previous commit (prev); GPU parity first.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
