@@ -457,6 +457,8 @@ def bench_mixed(args):
     timed_batches = [(first + i) % nb for i in range(args.steps)]
     single = None
     if len(engs) > 1:                                    # the same batches with engine 0 alone, for comparison
+        if link > 0:
+            engs[0].link(engs[1], 0)                     # (alone and unlinked: plain one-engine launches)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for bi in timed_batches:
