@@ -15,9 +15,9 @@ for n in 2048 4096 8192; do
   timeout -k 10 300 python bench.py --npkts $n --steps 40 --warmup 5 --no-cpu > gpurun_out/bench_n$n.log 2>&1 || { tail -5 gpurun_out/bench_n$n.log; exit 1; }
   tail -1 gpurun_out/bench_n$n.log | cut -c1-120
 done
-for a in "--config 1" "--config 2" "--config 5" "--eq" "--tx"; do
+for a in "--config 1" "--config 2" "--config 5 --steps 40" "--eq" "--tx"; do
   f=gpurun_out/bench_$(echo $a | tr -d ' -').log
-  timeout -k 10 300 python bench.py $a --steps 10 > $f 2>&1 || { echo "bench $a failed"; tail -5 $f; exit 1; }
+  timeout -k 10 300 python bench.py --steps 10 $a > $f 2>&1 || { echo "bench $a failed"; tail -5 $f; exit 1; }
   tail -1 $f | cut -c1-140
 done
 cd /tmp && export TMPDIR=/tmp && R=${GRAFT_REPO_ROOT:-/root/repo}
