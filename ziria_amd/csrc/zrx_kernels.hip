@@ -761,18 +761,28 @@ __global__ __launch_bounds__(256) void k_ofdm_eq(const uint4* __restrict__ sym, 
 //    lane's register is advanced past the 32*(63-L) bytes behind its chunk with two
 //    nibble-sliced zero-byte tables of its own (((63-L) & 7) x 32 and ((63-L) >> 3) x 256
 //    bytes: 16 lookups) and the wave XORs the 64 registers.
+//  * LDS layouts, for bank conflicts (ds_read_b32: 32 banks per 32 lanes; b128: 64 banks per
+//    16 lanes): the payload copy is indexed by v = i + 16 + u, u = (-c) & 7 for the chunk offset
+//    c = (plen - 2048) >> 2, so every lane's chunk starts at a multiple of 8 (v 0..15 static
+//    zeros, v 16..23 zeroed per packet before the payload lands) and is read by two ds_read_b128;
+//    v sits at v ^ (((v >> 6) & 1) << 2), which puts 16 consecutive chunks on 16 distinct 4-bank
+//    groups (unswizzled stride-8 words were 8-way conflicted).  The shift tables' rows are 144
+//    words apart so odd and even rows use opposite bank halves.
 constexpr int kCrcWaves = 8;
-constexpr int kCrcGuard = 8;                          // zero words before a wave's payload copy
+constexpr int kCrcGuard = 16;                         // static zero words (v) before a packet's copy
+constexpr int kCrcRegion = 544;                       // per wave: v 0 .. 534 (16 + 7 + 512 words)
+constexpr int kShfRow = 144;
+__device__ __forceinline__ int crc_lds_pos(int v) { return v ^ (((v >> 6) & 1) << 2); }
 __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t* __restrict__ dec,
                                                                    const int32_t* __restrict__ dec_bits,
                                                                    int32_t* __restrict__ info, uint8_t* __restrict__ payload,
                                                                    int npkts) {
   __shared__ uint32_t s4[4][256];
-  __shared__ uint32_t shf[16][128];                   // [n]: n * 32 zero bytes, [8 + n]: n * 256
+  __shared__ uint32_t shf[16][kShfRow];               // [n]: n * 32 zero bytes, [8 + n]: n * 256
   __shared__ uint32_t scrw2[256];                     // keystream words, doubled: [n] = kScrW[n mod 127]
   __shared__ uint8_t scrb[256];
   __shared__ uint8_t scrph[128];
-  __shared__ uint32_t pw_all[kCrcWaves][kCrcGuard + 512];   // per wave: zero guard, payload dwords
+  __shared__ __attribute__((aligned(16))) uint32_t pw_all[kCrcWaves][kCrcRegion];   // per wave: payload copy
   {                                                    // every table load in flight at once
     static_assert(64 * kCrcWaves == 512, "two words of each 1024-word table per thread");
     const int t = threadIdx.x;
@@ -783,16 +793,16 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
     const uint32_t d2 = kScrW[t < 127 ? t : t < 254 ? t - 127 : 0];
     const uint8_t e = kScrB2[min(t, 253)], f = kScrPhase[t & 127];
     (&s4[0][0])[t] = a0; (&s4[0][0])[t + 512] = a1;
-    (&shf[0][0])[t] = b0; (&shf[0][0])[t + 512] = b1;
-    (&shf[8][0])[t] = c0; (&shf[8][0])[t + 512] = c1;
+    shf[t >> 7][t & 127] = b0; shf[4 + (t >> 7)][t & 127] = b1;
+    shf[8 + (t >> 7)][t & 127] = c0; shf[12 + (t >> 7)][t & 127] = c1;
     if (t < 254) { scrw2[t] = d2; scrb[t] = e; }
     if (t < 128) scrph[t] = f;
-    if ((t & 63) < kCrcGuard) pw_all[t >> 6][t & 63] = 0u;
+    if ((t & 63) < kCrcGuard) pw_all[t >> 6][t & 63] = 0u;   // (v < 64: position = v)
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // (packet values below: scalar)
-  uint32_t* pw = pw_all[wv] + kCrcGuard;              // payload dword i at pw[i]; pw[-8 .. -1] = 0
+  uint32_t* pw = pw_all[wv];                          // v at pw[crc_lds_pos(v)]
   // grid-stride over packets (one wave per packet at a time): the LDS tables above are
   // staged once per block, not once per 8 packets.  Decoded bytes are read and payload
   // dwords written by buffer ops on the packet's own slot: 32-bit lane offsets, and a word
@@ -826,6 +836,11 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
     const uint32_t ksm = S == 0 ? 0u : 0xFFFFFFFFu;   // state 0 never leaves 0: zero keystream
     const int n0 = (16 * (int)scrph[S]) % 127;
     const uint32_t* ks = scrw2 + (n0 + 4 * lane) % 127;   // keystream word of dword lane + 64k: ks[2k]
+    const int c = (plen - 2048) >> 2;                  // payload word of lane 0's CRC chunk (floor)
+    const int u = (-c) & 7;
+    if (lane < 8) pw[16 + lane] = 0u;                  // v 16 .. 15 + u: zero (the rest: overwritten)
+    const int v0 = lane + kCrcGuard + u;               // v of dword lane + 64k: v0 + 64k
+    const int pe = crc_lds_pos(v0), po = pe ^ 4;       // its position, k even / odd
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       const int i = lane + 64 * k;
@@ -836,17 +851,21 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
       if (4 * (64 * k + 64) > plen)                    // (wave-uniform) bytes past the payload := 0
         v &= (uint32_t)(0xFFFFFFFFull >> (32 - 8 * min(max(plen - 4 * i, 0), 4)));
       __builtin_amdgcn_raw_buffer_store_b32(v, rp, 4 * i, 0, 0);   // (past the payload: dropped)
-      pw[i] = v;
+      pw[(k & 1 ? po : pe) + 64 * k] = v;
     }
     __builtin_amdgcn_wave_barrier();
     uint32_t crc;
     if (plen >= 4) {
-      const int q0 = 32 * lane - (2048 - plen);        // payload index of this lane's first byte
-      const int a = q0 >> 2;                           // (arithmetic: negative before the payload)
-      const int sh = q0 & 3;
-      uint32_t w[9];
-#pragma unroll
-      for (int j = 0; j < 9; j++) w[j] = pw[max(a + j, -kCrcGuard)];   // (before the payload: zeros)
+      // lane L's chunk: payload words 8L + c .. 8L + c + 8 at v = 8L + 16 + (c + u), a multiple
+      // of 8; a chunk wholly before v = 0 is all zeros, read from v 0..7.  Word 8 is word 0 of
+      // lane L + 1's chunk (lane 63: v = 528 + c + u, read by every lane as one broadcast).
+      const int vl = max(8 * lane + kCrcGuard + c + u, 0);
+      const int sh = plen & 3;                         // (byte offset of every lane's chunk)
+      const int p0 = crc_lds_pos(vl);
+      const uint4 lo = *(const uint4*)(pw + p0), hi = *(const uint4*)(pw + (p0 ^ 4));
+      const uint32_t last = pw[crc_lds_pos(528 + c + u)];
+      uint32_t w[9] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w, 0u};
+      w[8] = (uint32_t)__builtin_amdgcn_update_dpp((int)last, (int)lo.x, 0x130, 0xF, 0xF, false);
       uint32_t r = 0;
 #pragma unroll
       for (int j = 0; j < 8; j++) {
@@ -858,7 +877,7 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
       const uint32_t adv = 63u - (uint32_t)lane;
 #pragma unroll
       for (int k = 0; k < 2; k++) {
-        const uint32_t* tb2 = shf[k ? 8u + (adv >> 3) : (adv & 7u)];
+        const uint32_t* tb2 = shf[k ? 8u + (adv >> 3) : (adv & 7u)];   // (rows kShfRow apart)
         uint32_t t = 0;
 #pragma unroll
         for (int j = 0; j < 8; j++) t ^= tb2[j * 16 + ((r >> (4 * j)) & 15u)];
