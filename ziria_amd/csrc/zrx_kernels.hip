@@ -750,9 +750,10 @@ __global__ __launch_bounds__(256) void k_ofdm_eq(const uint4* __restrict__ sym, 
 //    one 127-periodic byte sequence read from phase 16*phase(S), so the payload is written
 //    with coalesced dword stores (256 B per store instruction).  Dword i = decoded bytes
 //    2+4i .. 5+4i: the upper neighbour word comes from lane + 1 by a wave_shl DPP move, the
-//    keystream word from a doubled table at a per-lane base (no wrap test), bytes past the
-//    payload are masked (one 64-bit shift, in the iterations that reach the payload's end).  The masked words also go to the wave's
-//    LDS region, behind 8 zero words.
+//    keystream word from a table indexed by 32 x byte offset mod 127 (4 x 32 = 1 mod 127, so
+//    consecutive lanes read consecutive words: no bank conflicts, no wrap test), bytes past the
+//    payload are masked (one 64-bit shift, in the iterations that reach the payload's end).
+//    The masked words also go to the wave's LDS copy (below).
 //  * CRC-32 check (crc.blk:85-118, = zlib): by linearity the reference's all-ones-initialised
 //    register is the zero-initialised one XOR kCrcOnes[n] (the all-ones value after n zero
 //    bytes), and leading zero bytes leave a zero register unchanged, so the payload is
@@ -779,7 +780,7 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
                                                                    int npkts) {
   __shared__ uint32_t s4[4][256];
   __shared__ uint32_t shf[16][kShfRow];               // [n]: n * 32 zero bytes, [8 + n]: n * 256
-  __shared__ uint32_t scrw2[256];                     // keystream words, doubled: [n] = kScrW[n mod 127]
+  __shared__ uint32_t scrw4[320];                     // keystream words: [j] = kScrW[4j mod 127]
   __shared__ uint8_t scrb[256];
   __shared__ uint8_t scrph[128];
   __shared__ __attribute__((aligned(16))) uint32_t pw_all[kCrcWaves][kCrcRegion];   // per wave: payload copy
@@ -790,12 +791,13 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
     const uint32_t* SL = &kCrcShiftLo[0][0];
     const uint32_t* SH = &kCrcShiftHi[0][0];
     const uint32_t a0 = S4[t], a1 = S4[t + 512], b0 = SL[t], b1 = SL[t + 512], c0 = SH[t], c1 = SH[t + 512];
-    const uint32_t d2 = kScrW[t < 127 ? t : t < 254 ? t - 127 : 0];
+    const uint32_t d2 = kScrW[(4 * t) % 127];
     const uint8_t e = kScrB2[min(t, 253)], f = kScrPhase[t & 127];
     (&s4[0][0])[t] = a0; (&s4[0][0])[t + 512] = a1;
     shf[t >> 7][t & 127] = b0; shf[4 + (t >> 7)][t & 127] = b1;
     shf[8 + (t >> 7)][t & 127] = c0; shf[12 + (t >> 7)][t & 127] = c1;
-    if (t < 254) { scrw2[t] = d2; scrb[t] = e; }
+    if (t < 320) scrw4[t] = d2;
+    if (t < 254) scrb[t] = e;
     if (t < 128) scrph[t] = f;
     if ((t & 63) < kCrcGuard) pw_all[t >> 6][t & 63] = 0u;   // (v < 64: position = v)
   }
@@ -835,7 +837,9 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
     const uint32_t S = ((uint32_t)__builtin_amdgcn_readfirstlane((int)wv9[0]) >> 9) & 0x7Fu;
     const uint32_t ksm = S == 0 ? 0u : 0xFFFFFFFFu;   // state 0 never leaves 0: zero keystream
     const int n0 = (16 * (int)scrph[S]) % 127;
-    const uint32_t* ks = scrw2 + (n0 + 4 * lane) % 127;   // keystream word of dword lane + 64k: ks[2k]
+    // keystream word of dword i = lane + 64k: kScrW[(n0 + 4i) mod 127] = scrw4[j] for j = 32 (n0 + 4i)
+    // mod 127 = (32 n0 mod 127) + lane + (64k mod 127): consecutive lanes, consecutive words
+    const uint32_t* ks = scrw4 + (4 * (int)scrph[S]) % 127 + lane;   // (32 n0 = 512 phase = 4 phase)
     const int c = (plen - 2048) >> 2;                  // payload word of lane 0's CRC chunk (floor)
     const int u = (-c) & 7;
     if (lane < 8) pw[16 + lane] = 0u;                  // v 16 .. 15 + u: zero (the rest: overwritten)
@@ -847,7 +851,7 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
       // dword i + 1: lane + 1's word k (wave_shl:1), lane 63's from lane 0's word k + 1
       const uint32_t up = (uint32_t)__builtin_amdgcn_readfirstlane((int)wv9[k + 1]);
       const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp((int)up, (int)wv9[k], 0x130, 0xF, 0xF, false);
-      uint32_t v = __builtin_amdgcn_alignbyte(nx, wv9[k], 2) ^ (ks[2 * k] & ksm);
+      uint32_t v = __builtin_amdgcn_alignbyte(nx, wv9[k], 2) ^ (ks[(k >> 1) + 64 * (k & 1)] & ksm);
       if (4 * (64 * k + 64) > plen)                    // (wave-uniform) bytes past the payload := 0
         v &= (uint32_t)(0xFFFFFFFFull >> (32 - 8 * min(max(plen - 4 * i, 0), 4)));
       __builtin_amdgcn_raw_buffer_store_b32(v, rp, 4 * i, 0, 0);   // (past the payload: dropped)
@@ -891,7 +895,7 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
       crc = ~crc;
     }
     if (lane == 0) {
-      const uint32_t rx = __builtin_amdgcn_alignbyte(t1, t0, (2 + plen) & 3) ^ (scrw2[(n0 + plen) % 127] & ksm);
+      const uint32_t rx = __builtin_amdgcn_alignbyte(t1, t0, (2 + plen) & 3) ^ (scrw4[(32 * (n0 + plen)) % 127] & ksm);
       in[4] = crc == rx ? 1 : 0;
     }
     __builtin_amdgcn_wave_barrier();                   // (this packet's LDS reads before the next one's writes)
