@@ -28,16 +28,20 @@ def _threads():
 
 def _check(oracle, b):
     n = b["sym_off"].numel()
+    chan = b.get("chan")
     e = RxEngine(0)
     try:
         e.reserve(n, b["max_nsym"])
-        pay, info = e.rx(b["sym"], b["sym_off"], b["nsym"], b["max_nsym"])
+        pay, info = e.rx(b["sym"], b["sym_off"], b["nsym"], b["max_nsym"], chan=chan)
         torch.cuda.synchronize()
         pay, info = pay.cpu().numpy(), info.cpu().numpy()
     finally:
         e.close()
-    opay, res = oracle.rx_batch_time_fast(b["sym"].cpu().numpy(), b["sym_off"].cpu().numpy(),
-                                          b["nsym"].cpu().numpy(), nthreads=_threads())
+    args = (b["sym"].cpu().numpy(), b["sym_off"].cpu().numpy(), b["nsym"].cpu().numpy())
+    if chan is None:
+        opay, res = oracle.rx_batch_time_fast(*args, nthreads=_threads())
+    else:
+        opay, res = oracle.rx_batch_time_eq_fast(*args, chan.cpu().numpy(), nthreads=_threads())
     hdr = np.array([(r["modulation"], r["coding"], r["len"], r["err"]) for r in res], np.int32)
     crc = np.array([r["crc_ok"] for r in res], np.int32)
     assert (info[:, :4] == hdr).all(), np.nonzero((info[:, :4] != hdr).any(1))[0][:10]
@@ -45,22 +49,36 @@ def _check(oracle, b):
     plen = np.maximum(hdr[:, 2] - 4, 0)
     bad = [i for i in range(n) if not hdr[i, 3] and not (pay[i, :plen[i]] == opay[i, :plen[i]]).all()]
     assert not bad, bad[:10]
-    return crc
+    return crc, pay
 
 
 def test_fullsize_config3_vs_port(oracle):
     b = txgen.make_batch(16384, seed=0x5EED, sigma=4.0, device="cuda")
-    crc = _check(oracle, b)
+    crc, _ = _check(oracle, b)
     assert crc.all()
 
 
 def test_fullsize_config3_noise_edge_vs_port(oracle):
     b = txgen.make_batch(16384, seed=58, sigma=58.0, device="cuda")
-    crc = _check(oracle, b)
+    crc, _ = _check(oracle, b)
     assert 0 < crc.sum() < crc.size                        # CRC failures do occur here
 
 
 def test_fullsize_config5_vs_port(oracle):
     m = txgen.make_mixed_fast(16384, min_len=64, max_len=4095, sigma=3.0, seed=0xC5C6, device="cuda")
-    crc = _check(oracle, m)
+    crc, _ = _check(oracle, m)
     assert crc.sum() > 7000
+
+
+@pytest.mark.parametrize("seed", [0x5EED, 0x5EEE])
+def test_fullsize_eq_bench_batches_vs_port(oracle, seed):
+    """The exact batches of `bench.py --eq` (FFT >>> ChannelEqualization >>> PilotTrack >>>
+    GetData, 3-tap channel + phase drift, AWGN sigma 2; seeds 0x5EED / 0x5EEE): header, CRC
+    verdict and payload of all 16384 packets against the port's EQ chain.  Some packets fail
+    their CRC at this noise level; every CRC-passing one must carry what was sent."""
+    b = txgen.make_batch_range(0, 16384, mod=3, coding=2, payload_len=1500, sigma=2.0, seed=seed,
+                               device="cuda", channel=True)
+    crc, pay = _check(oracle, b)
+    ok = crc == 1
+    assert 16000 < ok.sum() < 16384
+    assert (pay[ok, :1500] == b["payload"][ok]).all()

@@ -400,10 +400,32 @@ def test_chain_plan_reuse(engine):
             else:
                 assert info[i, 4] == 1 and (pay[i, :len(x["payload"][i])] == x["payload"][i]).all(), i
 
+    # a device-API Viterbi batch of the same packet count on the same engine between two equal
+    # rx batches: its plan replaces the rx plan, so the next rx batch must be planned afresh
+    g = torch.Generator(device="cuda")
+    g.manual_seed(95)
+    ns = 12048 // 24 * 48 + 48
+    vit = dict(soft=torch.randint(0, 8, (512 * ns,), generator=g, device="cuda", dtype=torch.int8),
+               soft_off=torch.arange(512, dtype=torch.int64, device="cuda") * ns,
+               params=torch.tensor([1000, 1, ns, 0], dtype=torch.int32, device="cuda").repeat(512, 1).contiguous(),
+               out_off=torch.arange(512, dtype=torch.int64, device="cuda") * 1024)
+
+    def run_vit(e):
+        out = torch.zeros(512 * 1024, dtype=torch.uint8, device="cuda")
+        bits = torch.zeros(512, dtype=torch.int32, device="cuda")
+        e.viterbi(vit["soft"], vit["soft_off"], vit["params"], out, vit["out_off"], bits)
+        return out, bits
+
     seq = [(a[0], a[0]["nsym"], ()), (a[1], a[1]["nsym"], ()), (a[0], a[0]["nsym"], ()), (b, b["nsym"], ()),
            (a[1], a[1]["nsym"], ()), (t, nsym_t, (200,)), (a[1], a[1]["nsym"], ()), (c, c["nsym"], ()),
-           (a[0], a[0]["nsym"], ())]
+           (a[0], a[0]["nsym"], ()), ("vit", None, ()), (a[0], a[0]["nsym"], ())]
     for x, nsym, bad in seq:
+        if x == "vit":
+            vo, vb = run_vit(engine)
+            fo, fb = run_vit(fresh)
+            torch.cuda.synchronize()
+            assert (vo == fo).all() and (vb == fb).all() and (vb == 8000).all()
+            continue
         pay, info = engine.rx(x["sym"], x["sym_off"], nsym, S)
         st = engine.plan_stats()
         pf, inf = fresh.rx(x["sym"], x["sym_off"], nsym, S)

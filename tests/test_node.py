@@ -161,3 +161,29 @@ def test_run_sharded_single_process():
                            lambda sh, k: None, lambda sh, b: (sh["p"], sh["i"]), _payload, steps=1, warmup=0,
                            payload_len=L)
     assert (res["lo"], res["hi"], res["ok"], res["packets"], res["payload_match"]) == (0, 5, 5, 5, True)
+
+
+def test_run_sharded_batches_keep_their_own_info():
+    """outputs() returns the decoder's live buffers (as bench.py's engine does), so batch 1's
+    decode overwrites batch 0's info; each batch's payload must still be judged against its
+    own CRC flags.  Batch 0 fails the CRC of packet 2 and leaves garbage there (a CRC-failing
+    packet's payload is not checked with crc_ok_only), batch 1 passes every packet."""
+    live = {"p": torch.zeros((5, 64), dtype=torch.uint8), "i": torch.zeros((5, 8), dtype=torch.int32)}
+
+    def decode(b):
+        live["p"][:, :L] = torch.from_numpy(_payload(0, 5, b))
+        live["i"][:, 2] = L + 4
+        live["i"][:, 4] = 1
+        if b == 0:
+            live["p"][2, :L] ^= 0x5A
+            live["i"][2, 4] = 0
+
+    def outputs(sh, b):
+        decode(b)
+        return live["p"], live["i"]
+
+    res = node.run_sharded(5, lambda lo, hi: live, lambda sh, k: decode(k % 2), outputs, _payload, steps=2,
+                           warmup=1, payload_len=L, crc_ok_only=True, nbatches=2)
+    assert res["ok"] == 9 and res["packets"] == 10
+    assert res["payload_match"] is True and res["mismatched_packets"] == 0
+    assert res["bits_per_batch"] == [4 * L * 8, 5 * L * 8]

@@ -485,6 +485,10 @@ int zrx_set_stream(zrx_ctx* c, void* stream) {
 
 int zrx_pipeline_link(zrx_ctx* a, zrx_ctx* b, int mode) {
   if (!a || !b || a == b || mode < 0 || mode > 7) return ZRX_EINVAL;
+  // the link orders two streams of one device (events without a system fence, the low-
+  // priority head stream beside the engine's own): both engines must be on it
+  if (a->device != b->device) return ZRX_EINVAL;
+  ZRX_CHECK(hipSetDevice(a->device));
   for (zrx_ctx* c : {a, b}) {
     if (c->peer && c->peer != a && c->peer != b) { c->peer->peer = nullptr; c->peer->link_mode = 0; }
     // stream-to-stream on one device: no system-scope fence (which writes back the L2s)

@@ -157,11 +157,15 @@ def run_sharded(total, make_shard, step, outputs, expected, steps, warmup, paylo
     gather_s = 0.0
     for b in range(nbatches):
         payload, info = outputs(shard, b)
+        # outputs() may hand back the engine's live buffers, which the next batch's decode
+        # overwrites; at world 1 gather_rows returns its argument itself, so keep copies of
+        # this batch's rows (the payload slice is a copy already, the info would not be)
+        payload, info = payload[:, :L].clone(), info.clone()
         ok, bits, _ = counts(info)
         _sync(device)
         tg = time.perf_counter()
-        ok_all, bits_all, _, pay_all = combine(ok, bits, 1, payload[:, :L].contiguous(), device=device)
-        info_all = gather_rows(info.contiguous())
+        ok_all, bits_all, _, pay_all = combine(ok, bits, 1, payload, device=device)
+        info_all = gather_rows(info)
         _sync(device)
         gather_s += time.perf_counter() - tg
         ok_b.append(ok_all)
