@@ -81,6 +81,9 @@ def main():
                          "mode 1) and for configs 2 and 5, else 1" % PIPELINE_BELOW)
     ap.add_argument("--link", type=int, default=-1, choices=[-1, 0, 1, 2, 3, 4, 5, 6, 7],
                     help="zrx_pipeline_link mode of two engines (-1: auto = 1 for configs 3/4, 4 for config 5)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="with --gpus N: every rank on GPU 0 over a gloo process group (the multi-rank path on a "
+                         "one-GPU box; functional, not a scaling point)")
     ap.add_argument("--batches", type=int, default=2,
                     help="distinct input batches per GPU the steps rotate through (config 3/4/5)")
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 5])
@@ -88,9 +91,14 @@ def main():
                     help="TX chain (transmitter() at 40 MHz, SURVEY §8f row 4) on config-3 packets")
     ap.add_argument("--eq", action="store_true",
                     help="config 3 through a channel, with ChannelEqualization + PilotTrack (SURVEY §8f row 1)")
+    ap.add_argument("--e2e", action="store_true",
+                    help="config 3 end to end from host memory through __ext_wifi_rx_batch (SURVEY §8d: kernel-only "
+                         "vs end-to-end incl. H2D from pinned memory)")
     args = ap.parse_args()
     if args.tx:
         return bench_tx(args)
+    if args.e2e:
+        return bench_e2e(args)
     if args.config == 1:
         return bench_capture(args)
     if args.config == 2:
@@ -106,19 +114,84 @@ def main():
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # --share-gpu: every rank on device 0, the process group over gloo (RCCL refuses two ranks
+    # on one device) -- the multi-rank path with the real engine on a one-GPU box; the ranks
+    # contend for one GPU, so its numbers are no scaling point
+    local = 0 if args.share_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.share_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
+    # The headline: config 3 at N = 1; at N > 1 the driver's SCALE command (no --total) is weak
+    # scaling, 16384 packets per rank.  The same N-rank run then also decodes config 4 as SURVEY
+    # §8(d) defines it -- config 3's 16384 packets split over the N ranks (strong scaling) --
+    # and reports it as "strong", so one SCALE invocation yields both.
+    head = rx_run(args, args.total if args.total else args.npkts * world, world, rank, local, dev)
+    strong = None
+    if world > 1 and not args.total:
+        strong = rx_run(args, args.npkts, world, rank, local, dev)
+
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        cpu = cpu_baseline(head["batch0"], args.cpu_seconds, head["batch0"].get("chan"))
+
+    if rank == 0:
+        line = {
+            "metric": "decoded Mbit/s (whole node) 802.11a 54Mbps RX, bit-exact, at 1/2/4/8 MI355X",
+            "value": head["value"],
+            "unit": "Mbit/s",
+            "n_gpus": 1 if args.share_gpu else world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": head["ms_per_step"],
+            "higher_is_better": True,
+            "scaling": "weak" if not args.total else "strong",
+            "vs_baseline": None,
+            "dtype": "int16+u8",
+            "data": ("synthetic (txgen.make_batch_range: random payloads, TX restated from transmitter.blk, "
+                     + ("3-tap channel + phase drift, AWGN sigma=2" if args.eq else "AWGN sigma=4")
+                     + f"; {args.batches} distinct batches per GPU, the steps rotate through them)"),
+            "config": head["config"],
+            "value_one_engine": head["value_one_engine"],
+            "bit_exact_check": head["bit_exact_check"],
+            "stage_ms": head["stage_ms"],
+            "stage_ms_from": "engine 0 alone over the rotating batches, HIP events, after the warmup and before "
+                             "the timed steps",
+            "roofline": head["roofline"],
+            "roofline_fft": head["roofline_fft"],
+            "gather_ms": head["gather_ms"],
+            "cpu_baseline": cpu,
+        }
+        if world > 1:
+            line["ranks"] = world
+        if args.share_gpu:
+            line["multi_rank_mode"] = (f"functional: {world} ranks share GPU 0, process group over gloo (host "
+                                       "copies); the ranks contend for one GPU, so this is no scaling point")
+        if strong is not None:
+            line["strong"] = {k: strong[k] for k in ("value", "ms_per_step", "value_one_engine", "bit_exact_check",
+                                                     "gather_ms")}
+            line["strong"].update(scaling="strong", config=strong["config"],
+                                  what="config 4 as SURVEY §8(d) defines it: config 3's 16384 packets split over "
+                                       f"the {world} ranks, timed in the same run after the weak-scaling headline")
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def rx_run(args, total, world, rank, local, dev):
+    """One N-rank measurement of the rx chain over a global batch of `total` packets
+    (node.run_sharded: every rank decodes its contiguous shard, rank 0 checks every gathered
+    packet).  Returns the line's per-run fields (rank 0's are complete)."""
     # ---------------------------------------------------------------- workload (HBM-resident)
     # One global batch (BASELINE config 4): packet i depends only on (seed, i), each rank
     # builds and decodes its contiguous shard, rank 0 checks every gathered packet.  Each rank
     # holds args.batches distinct such batches (seeds 0x5EED + b) and the steps rotate through
     # them, so no step re-reads samples the previous one left in the caches (MI355X's 256 MiB
     # Infinity Cache holds a whole 239 MB batch).
-    total = args.total if args.total else args.npkts * world
     sigma = 2.0 if args.eq else 4.0
     nb = args.batches
     lo, hi = node.shard_range(total, world, rank)
@@ -216,65 +289,45 @@ def main():
 
     value = res["bits"] * args.steps / elapsed / 1e6       # CRC-checked payload bits, all ranks
     ms_per_step = elapsed / args.steps * 1e3
-
-    # ---------------------------------------------------------------- CPU baseline (rank 0)
-    cpu = None
-    if rank == 0 and not args.no_cpu:
-        cpu = cpu_baseline(state["batches"][0], args.cpu_seconds, state["batches"][0].get("chan"))
-
+    out = {
+        "value": round(value, 1),
+        "ms_per_step": round(ms_per_step, 4),
+        "batch0": state["batches"][0],
+        "config": {"workload": f"config{'3+eq' if args.eq else ('4' if world > 1 else '3')}: {total} packets "
+                               f"({n} per GPU, contiguous shards) x {args.payload} B payload "
+                               f"@ 54 Mbps (64-QAM r3/4), {S} CP-removed complex16 OFDM symbols each, "
+                               "time-domain input resident in HBM"
+                               + (", FFT >>> ChannelEqualization >>> PilotTrack >>> GetData" if args.eq else ""),
+                   "packets_total": total, "packets_per_gpu": n, "payload_bytes": args.payload,
+                   "symbols_per_packet": S, "parallelism": f"packet-sharded x{world}",
+                   "batches_per_gpu": nb,
+                   "pipeline": f"{len(engs)} batch{'es' if len(engs) > 1 else ''} in flight"
+                               + (" (engines on separate streams, steps in turn, linked: a Viterbi starts after "
+                                  "the other batch's chain)" if len(engs) > 1 else "")},
+        "value_one_engine": round(res["bits"] * args.steps / single / 1e6, 1),
+        "stage_ms": {k: round(v, 4) for k, v in stage.items()},
+        "roofline": {"kernel": "k_viterbi3 (data Viterbi)", "bound": "valu",
+                     "achieved": round(achieved_tops, 3), "peak": round(VALU_PEAK_TOPS, 1),
+                     "unit": "Tops/s", "frac": round(achieved_tops / VALU_PEAK_TOPS, 4),
+                     "traffic": None if args.eq else traffic_for("k_viterbi3", n),
+                     "units": f"{OPS_PER_DECODED_BIT} int ops per decoded bit x {decoded_bits} bits/launch"},
+        "roofline_fft": {"kernel": "k_data_fft (FFT64+GetData+demap+deinterleave)", "bound": "hbm",
+                         "achieved": round(fft_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(fft_gbs / HBM_PEAK_GBS, 4),
+                         "traffic": None if args.eq else traffic_for("k_data_fft", n),
+                         "units": f"544 B per data symbol x {n * nsym_data} symbols/launch"},
+        "gather_ms": round(res["gather_s"] * 1e3, 3),
+    }
     if rank == 0:
-        line = {
-            "metric": "decoded Mbit/s (whole node) 802.11a 54Mbps RX, bit-exact, at 1/2/4/8 MI355X",
-            "value": round(value, 1),
-            "unit": "Mbit/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True,
-            "scaling": "weak" if not args.total else "strong",
-            "vs_baseline": None,
-            "dtype": "int16+u8",
-            "data": ("synthetic (txgen.make_batch_range: random payloads, TX restated from transmitter.blk, "
-                     + ("3-tap channel + phase drift, AWGN sigma=2" if args.eq else "AWGN sigma=4")
-                     + f"; {nb} distinct batches per GPU, the steps rotate through them)"),
-            "config": {"workload": f"config{'3+eq' if args.eq else ('4' if world > 1 else '3')}: {total} packets "
-                                   f"({n} per GPU, contiguous shards) x {args.payload} B payload "
-                                   f"@ 54 Mbps (64-QAM r3/4), {S} CP-removed complex16 OFDM symbols each, "
-                                   "time-domain input resident in HBM"
-                                   + (", FFT >>> ChannelEqualization >>> PilotTrack >>> GetData" if args.eq else ""),
-                       "packets_total": total, "packets_per_gpu": n, "payload_bytes": args.payload,
-                       "symbols_per_packet": S, "parallelism": f"packet-sharded x{world}",
-                       "batches_per_gpu": nb,
-                       "pipeline": f"{len(engs)} batch{'es' if len(engs) > 1 else ''} in flight"
-                                   + (" (engines on separate streams, steps in turn, linked: a Viterbi starts after "
-                                      "the other batch's chain)" if len(engs) > 1 else "")},
-            "value_one_engine": round(res["bits"] * args.steps / single / 1e6, 1),
-            "bit_exact_check": {"crc_pass": res["ok"], "packets": res["packets"],
-                                "payload_match": res["payload_match"],
-                                "mismatched_packets": res["mismatched_packets"],
-                                "pipeline_outputs_equal": state["outs_equal"],
-                                "checked_on": f"rank 0, every gathered packet of all {nb} batches vs its "
-                                              "transmitted payload"},
-            "stage_ms": {k: round(v, 4) for k, v in stage.items()},
-            "stage_ms_from": "engine 0 alone over the rotating batches, HIP events, after the warmup and before "
-                             "the timed steps",
-            "roofline": {"kernel": "k_viterbi3 (data Viterbi)", "bound": "valu",
-                         "achieved": round(achieved_tops, 3), "peak": round(VALU_PEAK_TOPS, 1),
-                         "unit": "Tops/s", "frac": round(achieved_tops / VALU_PEAK_TOPS, 4),
-                         "traffic": None if args.eq else traffic_for("k_viterbi3", n),
-                         "units": f"{OPS_PER_DECODED_BIT} int ops per decoded bit x {decoded_bits} bits/launch"},
-            "roofline_fft": {"kernel": "k_data_fft (FFT64+GetData+demap+deinterleave)", "bound": "hbm",
-                             "achieved": round(fft_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": round(fft_gbs / HBM_PEAK_GBS, 4),
-                             "traffic": None if args.eq else traffic_for("k_data_fft", n),
-                             "units": f"544 B per data symbol x {n * nsym_data} symbols/launch"},
-            "gather_ms": round(res["gather_s"] * 1e3, 3),
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+        out["bit_exact_check"] = {"crc_pass": res["ok"], "packets": res["packets"],
+                                  "payload_match": res["payload_match"],
+                                  "mismatched_packets": res["mismatched_packets"],
+                                  "pipeline_outputs_equal": state["outs_equal"],
+                                  "checked_on": f"rank 0, every gathered packet of all {nb} batches vs its "
+                                                "transmitted payload"}
+    for e in engs:
+        e.close()
+    return out
 
 
 def spawn_ranks(n):
@@ -509,6 +562,111 @@ def bench_mixed(args):
         "value_one_engine": round(bits * args.steps / single / 1e6, 1) if single else None,
         "stage_ms": {k: round(v, 4) for k, v in stage.items()},
         "cpu_baseline": cpu,
+    }), flush=True)
+
+
+PCIE5_X16_GBS = 32e9 * 16 * 128 / 130 / 8 / 1e9      # 63.0 GB/s per direction (PCIe 5.0 x16)
+
+
+def bench_e2e(args):
+    """SURVEY §8(d) "kernel-only vs end-to-end (incl. H2D from pinned memory) times": config 3
+    batches handed over in host memory to the drop-in's batched external __ext_wifi_rx_batch
+    (the call a wplc program makes: host arrays in, payload + info out, synchronous), which
+    cuts the batch into chunks and overlaps H2D, the chain and D2H (zrx_hostio.hpp).  Timed
+    three ways on the same batches: the device API with everything resident in HBM (the
+    headline's kernel-only path), the external from pinned host arrays (value), and from
+    pageable ones (numpy: the library copies through pinned slots with a worker pool).  The
+    link itself is measured by plain torch copies of one batch's samples and payload slots."""
+    dev = torch.device("cuda", 0)
+    n, nb, L = args.npkts, args.batches, args.payload
+    bs = [txgen.make_batch_range(0, n, mod=3, coding=2, payload_len=L, sigma=4.0, seed=0x5EED + j, device=dev)
+          for j in range(nb)]
+    S = bs[0]["max_nsym"]
+    csr = (np.arange(n + 1, dtype=np.int64) * S).astype(np.int32)
+    pin = [b["sym"].cpu().pin_memory() for b in bs]
+    page = [b["sym"].cpu().numpy().copy() for b in bs]
+    sym_bytes = pin[0].numel() * 2
+    outs = {"pinned": (torch.zeros((n, 4096), dtype=torch.uint8).pin_memory(),
+                       torch.zeros((n, 8), dtype=torch.int32).pin_memory()),
+            "pageable": (np.zeros((n, 4096), np.uint8), np.zeros((n, 8), np.int32))}
+    P = lambda a: C.c_void_p(a.data_ptr() if torch.is_tensor(a) else a.ctypes.data)
+    c_csr = P(csr)
+
+    def call(x, pay, info):
+        rc = zlib().__ext_wifi_rx_batch(P(x), S * n, c_csr, n + 1, P(pay), n * 4096 * 8, P(info), n * 8)
+        if rc < 0:
+            raise RuntimeError(f"__ext_wifi_rx_batch failed ({rc})")
+        return rc
+
+    def timed_calls(srcs, key):
+        pay, info = outs[key]
+        for k in range(args.warmup):
+            call(srcs[k % nb], pay, info)
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            call(srcs[k % nb], pay, info)
+        dt = time.perf_counter() - t0
+        good = True                                      # every batch once more, checked
+        for j in range(nb):
+            call(srcs[j], pay, info)
+            p, i = (pay.numpy(), info.numpy()) if torch.is_tensor(pay) else (pay, info)
+            good &= bool((i[:, 4] == 1).all()) and bool((p[:, :L] == bs[j]["payload"]).all())
+        return dt, good
+
+    # kernel-only: the device API on the same batches, resident in HBM
+    eng = RxEngine(0)
+    eng.reserve(n, S)
+    d_pay = torch.zeros((n, 4096), dtype=torch.uint8, device=dev)
+    d_info = torch.zeros((n, 8), dtype=torch.int32, device=dev)
+    it = {"k": 0}
+
+    def dstep():
+        b = bs[it["k"] % nb]
+        eng.rx(b["sym"], b["sym_off"], b["nsym"], S, d_pay, d_info)
+        it["k"] += 1
+    k_dt = _timed(dstep, args.steps, args.warmup)
+    # the link alone: one batch's samples up, its payload slots (what the external returns) down
+    d_sym = torch.empty_like(bs[0]["sym"])
+    h_pay = outs["pinned"][0]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    for _ in range(2):
+        ev[0].record()
+        for j in range(4):
+            d_sym.copy_(pin[j % nb], non_blocking=True)
+        ev[1].record()
+        for j in range(4):
+            h_pay.copy_(d_pay, non_blocking=True)
+        ev[2].record()
+        torch.cuda.synchronize()
+    h2d_gbs = 4 * sym_bytes / (ev[0].elapsed_time(ev[1]) * 1e-3) / 1e9
+    d2h_gbs = 4 * d_pay.numel() / (ev[1].elapsed_time(ev[2]) * 1e-3) / 1e9
+    p_dt, p_ok = timed_calls(pin, "pinned")
+    g_dt, g_ok = timed_calls(page, "pageable")
+    bits = n * L * 8
+    rate = lambda dt: round(bits * args.steps / dt / 1e6, 1)
+    bound = bits / (sym_bytes / (h2d_gbs * 1e9)) / 1e6      # payload Mbit/s if the link ran flat out
+    threads, host = host_cpus()
+    print(json.dumps({
+        "metric": "decoded Mbit/s end to end from host memory, 802.11a 54Mbps RX (config 3 via __ext_wifi_rx_batch)",
+        "value": rate(p_dt), "unit": "Mbit/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(p_dt / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int16+u8",
+        "data": f"synthetic (txgen.make_batch_range, AWGN sigma=4; {nb} batches, the steps rotate through them)",
+        "config": {"workload": f"config3: {n} packets x {L} B @ 54 Mbps, {S} symbols each, "
+                               f"{sym_bytes / 1e6:.1f} MB of samples per batch in host memory",
+                   "call": "__ext_wifi_rx_batch (synchronous: samples in, payload slots + info out)"},
+        "end_to_end": {"pinned_Mbps": rate(p_dt), "pageable_Mbps": rate(g_dt),
+                       "pinned_ms_per_batch": round(p_dt / args.steps * 1e3, 3),
+                       "pageable_ms_per_batch": round(g_dt / args.steps * 1e3, 3),
+                       "kernel_only_Mbps": rate(k_dt), "kernel_only_ms_per_batch": round(k_dt / args.steps * 1e3, 3)},
+        "link": {"h2d_GBps": round(h2d_gbs, 1), "d2h_GBps": round(d2h_gbs, 1), "peak_GBps": round(PCIE5_X16_GBS, 1),
+                 "h2d_frac": round(h2d_gbs / PCIE5_X16_GBS, 3),
+                 "h2d_bound_Mbps": round(bound, 1), "pinned_frac_of_h2d_bound": round(rate(p_dt) / bound, 3),
+                 "measured": "torch pinned->device copies of one batch's samples (x4), device->pinned of its "
+                             "payload slots (x4), HIP events"},
+        "bit_exact_check": {"pinned": p_ok, "pageable": g_ok,
+                            "checked": f"every packet of all {nb} batches: CRC pass and payload = sent"},
+        "host": dict(host, threads_available=threads),
     }), flush=True)
 
 

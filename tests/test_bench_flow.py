@@ -53,6 +53,8 @@ HARNESS = textwrap.dedent("""
             log.append(("new", self.id))
         def reserve(self, n, s):
             pass
+        def close(self):
+            log.append(("close", self.id))
         def link(self, other, mode):
             log.append(("link", self.id, other.id, mode))
         def plan_check(self):
@@ -172,6 +174,23 @@ def test_bench_gpus2_spawns_two_ranks(oracle, tmp_path):
     assert line["cpu_baseline"]["value"] > 0
     for r in (0, 1):
         assert any(e[0] == "rx" for e in logs[r])
+    # the same run also decodes config 4 as SURVEY §8(d) defines it: npkts packets in all,
+    # split over the ranks, every gathered packet checked
+    st = line["strong"]
+    assert st["scaling"] == "strong" and st["config"]["packets_total"] == 12 and st["config"]["packets_per_gpu"] == 6
+    assert st["bit_exact_check"]["packets"] == 2 * 12 and st["bit_exact_check"]["payload_match"] is True
+    assert st["value"] > 0 and st["ms_per_step"] > 0
+
+
+def test_bench_share_gpu_two_ranks(oracle, tmp_path):
+    """--share-gpu: both ranks on GPU 0 over a gloo group (the multi-rank path on a one-GPU
+    box): labelled as one GPU and no scaling point, every gathered packet checked."""
+    line, logs = _run(tmp_path, ["--gpus", "2", "--share-gpu", "--npkts", "10", "--steps", "2", "--warmup", "1",
+                                 "--no-cpu"])
+    assert sorted(logs) == [0, 1]
+    assert line["n_gpus"] == 1 and line["ranks"] == 2 and "no scaling point" in line["multi_rank_mode"]
+    assert line["bit_exact_check"]["packets"] == 2 * 20 and line["bit_exact_check"]["payload_match"] is True
+    assert line["strong"]["bit_exact_check"]["packets"] == 2 * 10
 
 
 def test_bench_one_engine_flow(oracle, tmp_path):

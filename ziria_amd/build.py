@@ -87,7 +87,7 @@ def build(force=False, verbose=False):
         subprocess.check_call(cmd, cwd=CSRC)
         objs.append(obj)
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-o", LIB + ".tmp", os.path.join(CSRC, "zrx_api.hip"), "-x", "none"] + objs
+           "-Wall", "-pthread", "-o", LIB + ".tmp", os.path.join(CSRC, "zrx_api.hip"), "-x", "none"] + objs
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd, cwd=CSRC)

@@ -20,6 +20,7 @@
 #include "../../include/ziria_rx.h"
 #include "zrx_internal.h"
 #include "zrx_kernels.hip"
+#include "zrx_hostio.hpp"
 
 using namespace zrx;
 
@@ -88,8 +89,9 @@ struct zrx_ctx {
   FftPlan* fft_plans = nullptr;
   uint32_t* fft_tw = nullptr;
   uint16_t* fft_pos = nullptr;
-  void* small = nullptr;          // staging of the batched externals' host arrays
+  void* small = nullptr;          // device buffers of the batched externals' host arrays
   size_t small_cap = 0;
+  zrx_io::HostIO* hio = nullptr;  // their copy streams and pinned slots (zrx_hostio.hpp)
   hipStream_t side = nullptr;     // k_pkt_rows beside k_data_fft (rx chain, mixed batches)
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int32_t* mixed_hint = nullptr;  // pinned, mapped: 1 when the last planned batch was mixed
@@ -456,6 +458,7 @@ int zrx_destroy(zrx_ctx* c) {
     (void)hipFree(p);
   for (void* p : {(void*)c->fft_plans, (void*)c->fft_tw, (void*)c->fft_pos}) (void)hipFree(p);
   (void)hipFree(c->small);
+  delete c->hio;
   if (c->mixed_hint) (void)hipHostFree(c->mixed_hint);
   for (auto& set : c->evsets)
     for (auto& e : set) (void)hipEventDestroy(e);
@@ -942,6 +945,44 @@ void sora_fft64_batch(struct complex16* out, int outlen, struct complex16* in, i
 }
 
 
+// The host pipelines' per-context state (zrx_hostio.hpp), created on first use.
+static zrx_io::HostIO* host_io(zrx_ctx* c) {
+  if (c->hio) return c->hio;
+  auto* io = new zrx_io::HostIO();
+  if (io->init(c->device) != hipSuccess) {
+    std::fprintf(stderr, "ziria_rx: copy streams / events for the host pipeline could not be created\n");
+    delete io;
+    return nullptr;
+  }
+  return c->hio = io;
+}
+
+// Waits for everything a host pipeline issued, on its error paths too: no copy into or out
+// of the caller's arrays may still be in flight when the call returns.
+static void host_io_quiesce(zrx_ctx* c) {
+  if (c->hio) {
+    (void)hipStreamSynchronize(c->hio->up);
+    (void)hipStreamSynchronize(c->hio->down);
+  }
+  (void)hipStreamSynchronize(c->stream);
+}
+
+// Plan words of the chunks (pinned: read back without a sync per chunk): any dropped row is
+// ZRX_EPLAN, never silent.
+static int plan_flags_ok(const zrx_io::HostIO* io, int nch) {
+  for (int j = 0; j < nch; j++)
+    if (io->flags[j] != 0) {
+      std::fprintf(stderr, "ziria_rx: the Viterbi plan dropped %d rows past its bound\n", io->flags[j]);
+      return ZRX_EPLAN;
+    }
+  return ZRX_OK;
+}
+
+// Packet i decodes soft[so[i] .. so[i+1]) and its bytes land at out_bits[pkt_out_off[i] ..].
+// The frames are decoded into a packed device buffer (frame i at the prefix of frame_len) and
+// only the bytes each frame produced (out_bits_count / 8: the brick emits whole bytes, window
+// by window) are scattered into the caller's array, whose other bytes stay as they were; so
+// the caller's output array is never uploaded.  Soft values go up in chunks (zrx_hostio.hpp).
 int32_t viterbi_batch_decode(const char* soft, int softlen, const int32_t* pkt_soft_off, int n_off,
                              const int32_t* frame_len, int n_fl, const int16_t* code_rate, int n_cr,
                              unsigned char* out_bits, int out_len_bits, const int32_t* pkt_out_off, int n_oo) {
@@ -950,7 +991,8 @@ int32_t viterbi_batch_decode(const char* soft, int softlen, const int32_t* pkt_s
   if (np == 0) return 0;
   const int64_t out_bytes = out_len_bits / 8;
   std::vector<int32_t> params(4 * (size_t)np);
-  std::vector<int64_t> soff(np), ooff(np);
+  std::vector<int64_t> soff(np), coff(np + 1);
+  coff[0] = 0;
   for (int i = 0; i < np; i++) {
     const int32_t n = pkt_soft_off[i + 1] - pkt_soft_off[i];
     const int cr = code_rate[i];
@@ -959,39 +1001,103 @@ int32_t viterbi_batch_decode(const char* soft, int softlen, const int32_t* pkt_s
       return ZRX_EINVAL;
     params[4 * i] = frame_len[i]; params[4 * i + 1] = cr; params[4 * i + 2] = n; params[4 * i + 3] = 0;
     soff[i] = pkt_soft_off[i];
-    ooff[i] = pkt_out_off[i];
+    coff[i + 1] = coff[i] + frame_len[i];
+  }
+  const std::vector<int> cut = zrx_io::chunk_cuts(
+      np, [&](int i) { return (size_t)(pkt_soft_off[i + 1] - pkt_soft_off[i]); },
+      (size_t)(pkt_soft_off[np] - pkt_soft_off[0]));
+  const int nch = (int)cut.size() - 1;
+  int maxn = 0;
+  size_t in_max = 0, out_max = 0;
+  for (int j = 0; j < nch; j++) {
+    const int n = cut[j + 1] - cut[j];
+    maxn = std::max(maxn, n);
+    in_max = std::max(in_max, (size_t)(pkt_soft_off[cut[j + 1]] - pkt_soft_off[cut[j]]));
+    out_max = std::max(out_max, (size_t)n * 4 + (size_t)(coff[cut[j + 1]] - coff[cut[j]]));
   }
   std::lock_guard<std::mutex> lk(g_mu);
   zrx_ctx* c = default_ctx();
   if (!c) return ZRX_ENODEV;
-  int rc0 = zrx_reserve(c, np, 1);                   // room for the row plan of k_pkt_plan
-  if (rc0) return rc0;
-  const size_t s_soft = ((size_t)softlen + 255) / 256 * 256, s_par = (size_t)np * 16, s_off = (size_t)np * 8;
-  const size_t s_out = ((size_t)out_bytes + 255) / 256 * 256;
-  uint8_t* d = (uint8_t*)staging(c, s_soft + s_par + 2 * s_off + s_out + (size_t)np * 4 + 1024);
+  int rc = zrx_reserve(c, maxn, 1);                  // room for the row plan of k_pkt_plan
+  if (rc) return rc;
+  zrx_io::HostIO* io = host_io(c);
+  if (!io) return ZRX_EHIP;
+  const auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+  const size_t s_soft = al((size_t)softlen), s_par = al((size_t)np * 16), s_off = al((size_t)np * 8);
+  const size_t s_out = al((size_t)coff[np]);
+  uint8_t* d = (uint8_t*)staging(c, s_soft + s_par + 2 * s_off + s_out + al((size_t)np * 4));
   if (!d) return ZRX_ENOMEM;
   uint8_t* d_soft = d;
   int32_t* d_par = (int32_t*)(d_soft + s_soft);
-  int64_t* d_soff = (int64_t*)((uint8_t*)d_par + ((s_par + 255) / 256) * 256);
-  int64_t* d_ooff = (int64_t*)((uint8_t*)d_soff + ((s_off + 255) / 256) * 256);
-  uint8_t* d_out = (uint8_t*)d_ooff + ((s_off + 255) / 256) * 256;
+  int64_t* d_soff = (int64_t*)((uint8_t*)d_par + s_par);
+  int64_t* d_coff = (int64_t*)((uint8_t*)d_soff + s_off);
+  uint8_t* d_out = (uint8_t*)d_coff + s_off;
   int32_t* d_bits = (int32_t*)(d_out + s_out);
-  ZRX_CHECK(hipMemcpyAsync(d_soft, soft, (size_t)softlen, hipMemcpyHostToDevice, c->stream));
-  ZRX_CHECK(hipMemcpyAsync(d_par, params.data(), s_par, hipMemcpyHostToDevice, c->stream));
-  ZRX_CHECK(hipMemcpyAsync(d_soff, soff.data(), s_off, hipMemcpyHostToDevice, c->stream));
-  ZRX_CHECK(hipMemcpyAsync(d_ooff, ooff.data(), s_off, hipMemcpyHostToDevice, c->stream));
-  ZRX_CHECK(hipMemcpyAsync(d_out, out_bits, (size_t)out_bytes, hipMemcpyHostToDevice, c->stream));
-  int rc = zrx_viterbi_dev(c, (const int8_t*)d_soft, d_soff, d_par, np, d_out, d_ooff, d_bits);
+  const bool pin_in = zrx_io::is_pinned(soft + pkt_soft_off[0], (size_t)(pkt_soft_off[np] - pkt_soft_off[0]));
+  if ((!pin_in && io->reserve_in(in_max) != hipSuccess) || io->reserve_out(out_max) != hipSuccess ||
+      io->reserve_flags(nch) != hipSuccess)
+    return ZRX_ENOMEM;
+  auto run = [&]() -> int {
+    ZRX_CHECK(hipMemcpyAsync(d_par, params.data(), (size_t)np * 16, hipMemcpyHostToDevice, io->up));
+    ZRX_CHECK(hipMemcpyAsync(d_soff, soff.data(), (size_t)np * 8, hipMemcpyHostToDevice, io->up));
+    ZRX_CHECK(hipMemcpyAsync(d_coff, coff.data(), (size_t)np * 8, hipMemcpyHostToDevice, io->up));
+    // chunk j's outputs, staged in out slot j & 1: packed bytes, then the bit counts
+    auto drain = [&](int j) -> int {
+      const int slot = j & 1, p0 = cut[j], p1 = cut[j + 1];
+      ZRX_CHECK(hipEventSynchronize(io->down_done[slot]));
+      const uint8_t* bytes = io->out[slot];
+      const int32_t* bits = (const int32_t*)(bytes + (size_t)(coff[p1] - coff[p0]));
+      io->pool->run((p1 - p0 + 255) / 256, [&](int t) {
+        for (int i = p0 + 256 * t; i < std::min(p1, p0 + 256 * (t + 1)); i++) {
+          const int nb = std::min<int>(frame_len[i], (std::max(bits[i - p0], 0) + 7) / 8);
+          std::memcpy(out_bits + pkt_out_off[i], bytes + (coff[i] - coff[p0]), (size_t)nb);
+        }
+      });
+      return ZRX_OK;
+    };
+    for (int j = 0; j < nch; j++) {
+      const int slot = j & 1, p0 = cut[j], p1 = cut[j + 1], n = p1 - p0;
+      const size_t s0 = (size_t)pkt_soft_off[p0], sb = (size_t)(pkt_soft_off[p1] - pkt_soft_off[p0]);
+      const char* src = soft + s0;
+      if (!pin_in) {
+        ZRX_CHECK(hipEventSynchronize(io->up_done[slot]));   // the slot's last upload is done
+        zrx_io::par_copy(*io->pool, io->in[slot], src, sb);
+        src = (const char*)io->in[slot];
+      }
+      if (sb) ZRX_CHECK(hipMemcpyAsync(d_soft + s0, src, sb, hipMemcpyHostToDevice, io->up));
+      ZRX_CHECK(hipEventRecord(io->up_done[slot], io->up));
+      ZRX_CHECK(hipStreamWaitEvent(c->stream, io->up_done[slot], 0));
+      const int r = zrx_viterbi_dev(c, (const int8_t*)d_soft, d_soff + p0, d_par + 4 * (size_t)p0, n, d_out,
+                                    d_coff + p0, d_bits + p0);
+      if (r) return r;
+      ZRX_CHECK(hipMemcpyAsync(io->flags + j, c->nrows + v3::kPlanDropped, 4, hipMemcpyDeviceToHost, c->stream));
+      ZRX_CHECK(hipEventRecord(io->decoded, c->stream));
+      ZRX_CHECK(hipStreamWaitEvent(io->down, io->decoded, 0));
+      const size_t ob = (size_t)(coff[p1] - coff[p0]);
+      if (ob) ZRX_CHECK(hipMemcpyAsync(io->out[slot], d_out + coff[p0], ob, hipMemcpyDeviceToHost, io->down));
+      ZRX_CHECK(hipMemcpyAsync(io->out[slot] + ob, d_bits + p0, (size_t)n * 4, hipMemcpyDeviceToHost, io->down));
+      ZRX_CHECK(hipEventRecord(io->down_done[slot], io->down));
+      if (j >= 1) {
+        const int r2 = drain(j - 1);                   // (overlaps chunk j's transfers and decode)
+        if (r2) return r2;
+      }
+    }
+    return drain(nch - 1);
+  };
+  rc = run();
+  host_io_quiesce(c);
   if (rc) return rc;
-  ZRX_CHECK(hipMemcpyAsync(out_bits, d_out, (size_t)out_bytes, hipMemcpyDeviceToHost, c->stream));
-  ZRX_CHECK(hipStreamSynchronize(c->stream));
-  rc = zrx_plan_check(c);                            // rows dropped by the plan: ZRX_EPLAN, never silent
+  rc = plan_flags_ok(io, nch);
   return rc ? rc : np;
 }
 
 
 // receiveBits over host packets; chan (64 coefficients per packet, chan_len >= 64 npkts) adds
-// ChannelEqualization + PilotTrack
+// ChannelEqualization + PilotTrack.  Chunks of whole packets are uploaded, decoded and
+// downloaded in a pipeline (zrx_hostio.hpp); a chunk's payload slots come back `cw` bytes
+// wide: the most a packet of that chunk can carry (LENGTH - 4 <= 27 x data symbols - 6 at
+// 54 Mbps, 216 bits a symbol for LENGTH + 2 decoded bytes; <= 2044 since LENGTH <= 2048),
+// which k_descramble_crc writes in whole dwords after the chunk's memset zeroes them.
 int32_t wifi_rx_batch(struct complex16* sym, int nsym_total, const int32_t* pkt_sym_off, int n_off,
                       const struct complex16* chan, int chan_len, unsigned char* payload, int payload_len_bits,
                       int32_t* pkt_info, int n_info) {
@@ -1009,34 +1115,105 @@ int32_t wifi_rx_batch(struct complex16* sym, int nsym_total, const int32_t* pkt_
     ns[i] = pkt_sym_off[i + 1] - pkt_sym_off[i];
     max_ns = std::max(max_ns, ns[i]);
   }
+  const size_t cb = chan ? 256 : 0;                  // channel bytes per packet
+  const std::vector<int> cut = zrx_io::chunk_cuts(np, [&](int i) { return (size_t)ns[i] * 256 + cb; },
+                                                   (size_t)(pkt_sym_off[np] - pkt_sym_off[0]) * 256 + cb * np);
+  const int nch = (int)cut.size() - 1;
+  std::vector<int> cmax(nch, 1), cw(nch, 0);
+  int maxn = 0;
+  size_t in_max = 0, out_max = 0;
+  for (int j = 0; j < nch; j++) {
+    const int n = cut[j + 1] - cut[j];
+    for (int i = cut[j]; i < cut[j + 1]; i++) cmax[j] = std::max(cmax[j], ns[i]);
+    cw[j] = (std::min(2044, std::max(27 * (cmax[j] - 1) - 6, 0)) + 3) & ~3;
+    maxn = std::max(maxn, n);
+    in_max = std::max(in_max, (size_t)(pkt_sym_off[cut[j + 1]] - pkt_sym_off[cut[j]]) * 256 + cb * n);
+    out_max = std::max(out_max, (size_t)n * 32 + (size_t)n * cw[j]);
+  }
   std::lock_guard<std::mutex> lk(g_mu);
   zrx_ctx* c = default_ctx();
   if (!c) return ZRX_ENODEV;
-  int rc = zrx_reserve(c, np, max_ns);
+  int rc = zrx_reserve(c, maxn, max_ns);
   if (rc) return rc;
-  const size_t s_sym = ((size_t)nsym_total * 256 + 255) / 256 * 256 + 256;
-  const size_t s_off = ((size_t)np * 8 + 255) / 256 * 256, s_ns = ((size_t)np * 4 + 255) / 256 * 256;
-  const size_t s_pay = (size_t)np * kPayloadStride, s_info = (size_t)np * 32;
-  const size_t s_chan = chan ? (size_t)np * 256 : 0;
-  uint8_t* d = (uint8_t*)staging(c, s_sym + s_off + s_ns + s_pay + s_info + s_chan + 1024);
+  zrx_io::HostIO* io = host_io(c);
+  if (!io) return ZRX_EHIP;
+  const auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+  const size_t s_sym = al((size_t)pkt_sym_off[np] * 256) + 256;
+  const size_t s_off = al((size_t)np * 8), s_ns = al((size_t)np * 4);
+  const size_t s_pay = (size_t)np * kPayloadStride, s_info = al((size_t)np * 32);
+  const size_t s_chan = (size_t)np * cb;
+  uint8_t* d = (uint8_t*)staging(c, s_sym + s_off + s_ns + s_pay + s_info + s_chan);
   if (!d) return ZRX_ENOMEM;
   uint8_t* d_sym = d;
   int64_t* d_off = (int64_t*)(d + s_sym);
   int32_t* d_ns = (int32_t*)((uint8_t*)d_off + s_off);
   uint8_t* d_pay = (uint8_t*)d_ns + s_ns;
   int32_t* d_info = (int32_t*)(d_pay + s_pay);
-  struct complex16* d_chan = chan ? (struct complex16*)((uint8_t*)d_info + (s_info + 255) / 256 * 256) : nullptr;
-  if (chan) ZRX_CHECK(hipMemcpyAsync(d_chan, chan, s_chan, hipMemcpyHostToDevice, c->stream));
-  ZRX_CHECK(hipMemcpyAsync(d_sym, sym, (size_t)nsym_total * 256, hipMemcpyHostToDevice, c->stream));
-  ZRX_CHECK(hipMemcpyAsync(d_off, off.data(), (size_t)np * 8, hipMemcpyHostToDevice, c->stream));
-  ZRX_CHECK(hipMemcpyAsync(d_ns, ns.data(), (size_t)np * 4, hipMemcpyHostToDevice, c->stream));
-  ZRX_CHECK(hipMemsetAsync(d_pay, 0, s_pay, c->stream));
-  rc = rx_chain(c, (const complex16*)d_sym, d_off, d_ns, np, max_ns, d_chan, d_pay, d_info);
+  uint8_t* d_chan = (uint8_t*)d_info + s_info;
+  const uint8_t* hs = (const uint8_t*)sym;
+  const bool pin_in = zrx_io::is_pinned(hs + (size_t)pkt_sym_off[0] * 256,
+                                        (size_t)(pkt_sym_off[np] - pkt_sym_off[0]) * 256) &&
+                      (!chan || zrx_io::is_pinned(chan, (size_t)np * 256));
+  const bool pin_out = zrx_io::is_pinned(payload, (size_t)np * kPayloadStride) &&
+                       zrx_io::is_pinned(pkt_info, (size_t)np * 32);
+  if ((!pin_in && io->reserve_in(in_max) != hipSuccess) || (!pin_out && io->reserve_out(out_max) != hipSuccess) ||
+      io->reserve_flags(nch) != hipSuccess)
+    return ZRX_ENOMEM;
+  auto run = [&]() -> int {
+    ZRX_CHECK(hipMemcpyAsync(d_off, off.data(), (size_t)np * 8, hipMemcpyHostToDevice, io->up));
+    ZRX_CHECK(hipMemcpyAsync(d_ns, ns.data(), (size_t)np * 4, hipMemcpyHostToDevice, io->up));
+    // chunk j's outputs, staged in out slot j & 1 (pageable caller arrays): info, then the
+    // payload slots packed cw[j] bytes apart
+    auto drain = [&](int j) -> int {
+      const int slot = j & 1, p0 = cut[j], n = cut[j + 1] - p0;
+      ZRX_CHECK(hipEventSynchronize(io->down_done[slot]));
+      std::memcpy(pkt_info + 8 * (size_t)p0, io->out[slot], (size_t)n * 32);
+      zrx_io::par_copy_2d(*io->pool, payload + (size_t)p0 * kPayloadStride, kPayloadStride,
+                          io->out[slot] + (size_t)n * 32, cw[j], cw[j], n);
+      return ZRX_OK;
+    };
+    for (int j = 0; j < nch; j++) {
+      const int slot = j & 1, p0 = cut[j], p1 = cut[j + 1], n = p1 - p0;
+      const size_t s0 = (size_t)pkt_sym_off[p0] * 256, sb = (size_t)(pkt_sym_off[p1] - pkt_sym_off[p0]) * 256;
+      const uint8_t* src = hs + s0;
+      const uint8_t* csrc = chan ? (const uint8_t*)chan + (size_t)p0 * 256 : nullptr;
+      if (!pin_in) {
+        ZRX_CHECK(hipEventSynchronize(io->up_done[slot]));   // the slot's last upload is done
+        zrx_io::par_copy(*io->pool, io->in[slot], src, sb);
+        if (chan) std::memcpy(io->in[slot] + sb, csrc, (size_t)n * 256);
+        src = io->in[slot];
+        csrc = io->in[slot] + sb;
+      }
+      if (sb) ZRX_CHECK(hipMemcpyAsync(d_sym + s0, src, sb, hipMemcpyHostToDevice, io->up));
+      if (chan) ZRX_CHECK(hipMemcpyAsync(d_chan + (size_t)p0 * 256, csrc, (size_t)n * 256, hipMemcpyHostToDevice, io->up));
+      ZRX_CHECK(hipEventRecord(io->up_done[slot], io->up));
+      ZRX_CHECK(hipStreamWaitEvent(c->stream, io->up_done[slot], 0));
+      uint8_t* dp = d_pay + (size_t)p0 * kPayloadStride;
+      if (cw[j]) ZRX_CHECK(hipMemset2DAsync(dp, kPayloadStride, 0, cw[j], n, c->stream));
+      const int r = rx_chain(c, (const complex16*)d_sym, d_off + p0, d_ns + p0, n, cmax[j],
+                             chan ? (const complex16*)(d_chan + (size_t)p0 * 256) : nullptr, dp, d_info + 8 * (size_t)p0);
+      if (r) return r;
+      ZRX_CHECK(hipMemcpyAsync(io->flags + j, c->nrows + v3::kPlanDropped, 4, hipMemcpyDeviceToHost, c->stream));
+      ZRX_CHECK(hipEventRecord(io->decoded, c->stream));
+      ZRX_CHECK(hipStreamWaitEvent(io->down, io->decoded, 0));
+      uint8_t* oi = pin_out ? (uint8_t*)(pkt_info + 8 * (size_t)p0) : io->out[slot];
+      uint8_t* op = pin_out ? payload + (size_t)p0 * kPayloadStride : io->out[slot] + (size_t)n * 32;
+      ZRX_CHECK(hipMemcpyAsync(oi, d_info + 8 * (size_t)p0, (size_t)n * 32, hipMemcpyDeviceToHost, io->down));
+      if (cw[j])
+        ZRX_CHECK(hipMemcpy2DAsync(op, pin_out ? (size_t)kPayloadStride : (size_t)cw[j], dp, kPayloadStride, cw[j], n,
+                                   hipMemcpyDeviceToHost, io->down));
+      ZRX_CHECK(hipEventRecord(io->down_done[slot], io->down));
+      if (!pin_out && j >= 1) {
+        const int r2 = drain(j - 1);                   // (overlaps chunk j's transfers and decode)
+        if (r2) return r2;
+      }
+    }
+    return pin_out ? ZRX_OK : drain(nch - 1);
+  };
+  rc = run();
+  host_io_quiesce(c);
   if (rc) return rc;
-  ZRX_CHECK(hipMemcpyAsync(payload, d_pay, s_pay, hipMemcpyDeviceToHost, c->stream));
-  ZRX_CHECK(hipMemcpyAsync(pkt_info, d_info, s_info, hipMemcpyDeviceToHost, c->stream));
-  ZRX_CHECK(hipStreamSynchronize(c->stream));
-  rc = zrx_plan_check(c);                            // rows dropped by the plan: ZRX_EPLAN, never silent
+  rc = plan_flags_ok(io, nch);
   if (rc) return rc;
   int ok = 0;
   for (int i = 0; i < np; i++) ok += pkt_info[8 * i + 4] != 0;

@@ -809,17 +809,28 @@ __global__ __launch_bounds__(64 * kCrcWaves) void k_descramble_crc(const uint8_t
   // staged once per block, not once per 8 packets.  Decoded bytes are read and payload
   // dwords written by buffer ops on the packet's own slot: 32-bit lane offsets, and a word
   // outside the slot (load: 0) or past the payload (store: dropped) needs no branch.
-  for (int p = blockIdx.x * kCrcWaves + wv; p < npkts; p += gridDim.x * kCrcWaves) {
+  // Each packet's LENGTH is read one packet ahead (the first one before the tables are staged),
+  // so its slot loads can stop at the decoded bytes the packet has: len + 2, plus the next
+  // dword the descrambler aligns against (the slot is kDecStride = 2080 bytes; reading it all
+  // fetched 1.42x the bytes a config-3 packet needs).
+  int p = blockIdx.x * kCrcWaves + wv;
+  int len_next = p < npkts ? info[8 * (int64_t)p + 2] : 0;
+  for (; p < npkts; p += gridDim.x * kCrcWaves) {
     int32_t* in = info + 8 * (int64_t)p;
     const uint8_t* d = dec + (int64_t)p * kDecStride;
-    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)d, (short)0, kDecStride, 0x00020000);
+    const int len = len_next;
+    const int pn = p + gridDim.x * kCrcWaves;
+    if (pn < npkts) len_next = info[8 * (int64_t)pn + 2];
+    const int nrec = min(kDecStride, (max(len, 0) + 2 + 4 + 3) & ~3);
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)d, (short)0, nrec, 0x00020000);
     // payload: dword i = decoded bytes 2+4i .. 5+4i.  The lane's dwords i = lane + 64k
     // (k < 8: plen <= 2044) are loaded with the header fields, before any of them is looked at
-    // (a packet that turns out to have no payload wastes them).
+    // (a packet that turns out to have no payload wastes them; loads past nrec read 0 and
+    // fetch nothing).
     uint32_t wv9[9];
 #pragma unroll
     for (int k = 0; k < 9; k++) wv9[k] = __builtin_amdgcn_raw_buffer_load_b32(rd, 4 * (lane + 64 * k), 0, 0);
-    const int len = in[2], status = in[5];
+    const int status = in[5];
     const int bits = dec_bits[p];
     if (lane == 0) in[7] = bits;
     if (status != 0 || bits < (len + 2) * 8 || len < 4) {

@@ -26,6 +26,14 @@ def world_rank():
     return 1, 0
 
 
+def comm_device(device=None):
+    """Where collective tensors live: the GPU for RCCL ("nccl"), the host for gloo (the CPU
+    tests, and bench.py --share-gpu, where the ranks share one GPU)."""
+    if dist.is_initialized() and dist.get_backend() == "gloo":
+        return torch.device("cpu")
+    return device
+
+
 def shard_range(npkts, world, rank):
     """Contiguous [start, stop) packet range of `rank`; sizes differ by at most one."""
     if world < 1 or not 0 <= rank < world or npkts < 0:
@@ -79,7 +87,7 @@ def combine(ok, bits, match, payload=None, dst=0, device=None):
     world, _ = world_rank()
     if world == 1:
         return ok, bits, match, payload
-    t = torch.tensor([ok, bits, match], dtype=torch.int64, device=device)
+    t = torch.tensor([ok, bits, match], dtype=torch.int64, device=comm_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     gathered = gather_rows(payload, dst) if payload is not None else None
     o, b, m = (int(v) for v in t.tolist())
@@ -91,7 +99,7 @@ def max_over_ranks(seconds, device=None):
     world, _ = world_rank()
     if world == 1:
         return seconds
-    t = torch.tensor([seconds], dtype=torch.float64, device=device)
+    t = torch.tensor([seconds], dtype=torch.float64, device=comm_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -161,6 +169,9 @@ def run_sharded(total, make_shard, step, outputs, expected, steps, warmup, paylo
         # overwrites; at world 1 gather_rows returns its argument itself, so keep copies of
         # this batch's rows (the payload slice is a copy already, the info would not be)
         payload, info = payload[:, :L].clone(), info.clone()
+        cd = comm_device(device)
+        if cd is not None:
+            payload, info = payload.to(cd), info.to(cd)
         ok, bits, _ = counts(info)
         _sync(device)
         tg = time.perf_counter()
