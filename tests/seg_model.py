@@ -5,15 +5,17 @@ kernel's packed layout.  tests/test_seg_model.py checks it against the oracle's 
 decode (oracle/ziria_oracle.c zo_vit_decode = csrc/sora_ext_viterbi.cpp:66-153), so the
 seam argument is proven on the CPU before the kernel runs it.
 
-Geometry (same formulas as v3::seg_start / seg_count / seg_stop):
-  S_k = 768 * round(k E / (nseg 768))   segment k's first column (k >= 1; S_0 = 0)
-  J_k = S_k + 256                       first output bit of segment k
-  C_k = S_k + 240                       seam column: both sides' metrics compared here
-  segment k - 1 stops at J_k + 30        (its window at ob = J_k - 256 has then fired)
+Geometry (same formulas as v3::seg_start / seg_count / seg_stop), warm-up W = 256 (mixed
+batches) or 136 (uniform batches, v3::kSegWarmUni):
+  J_k = 768 * round(k E / (nseg 768)) + 256   first output bit of segment k (k >= 1)
+  S_k = J_k - W                                segment k's first column (S_0 = 0)
+  C_k = S_k + W - 16                           seam column: both sides' metrics compared here
+  segment k - 1 stops at J_k + 30              (its window at ob = J_k - 256 has then fired)
 """
 import numpy as np
 
 UNIT, WARM, CMP, MAX_SEG, MIN_SEG, MIN_CUT, MAX_END = 768, 256, 240, 8, 1536, 1024, 1 << 24
+WARM_UNI = 136
 PREFIX, LOOK, DEPTH = 6, 24, 256
 
 _S = np.arange(64)
@@ -41,8 +43,8 @@ def _bm(v, e):
     return np.where(e, 14 - 2 * v, 2 * v)
 
 
-def seg_start(E, nseg, k):
-    return 0 if k == 0 else UNIT * ((2 * k * E + nseg * UNIT) // (2 * nseg * UNIT))
+def seg_start(E, nseg, k, warm=WARM):
+    return 0 if k == 0 else UNIT * ((2 * k * E + nseg * UNIT) // (2 * nseg * UNIT)) + WARM - warm
 
 
 def seg_count(E, cols, L, min_len=MIN_SEG):
@@ -54,8 +56,8 @@ def seg_count(E, cols, L, min_len=MIN_SEG):
     return min(max(n, 1), MAX_SEG)
 
 
-def seg_stop(E, cols, nseg, k):
-    return seg_start(E, nseg, k + 1) + WARM + 30 if k + 1 < nseg else cols
+def seg_stop(E, cols, nseg, k, warm=WARM):
+    return seg_start(E, nseg, k + 1, warm) + warm + 30 if k + 1 < nseg else cols
 
 
 def order_place(pos, nfull, ncu, rows=32):
@@ -164,27 +166,28 @@ def decode_range(soft, cr, fl, S, m0, ob0, stop, dump_cols=(), cmp=None):
     return out, dumps, stop
 
 
-def segmented_decode(soft, cr, fl, nseg):
+def segmented_decode(soft, cr, fl, nseg, warm=WARM):
     """Pass 1 over the nseg segments, the seam check, the fix pass; returns (bytes, number
     of fix rows run)."""
     E = 8 * fl + PREFIX
+    cmpc = warm - 16
     cols = cols_of(cr, len(soft))
     out = {}
     A, B = {}, {}                                        # seam j: side A (segment j-1), side B (segment j)
     for k in range(nseg):
-        S = seg_start(E, nseg, k)
+        S = seg_start(E, nseg, k, warm)
         dc = set()
         if k:
-            dc.add(S + CMP)
+            dc.add(S + cmpc)
         if k + 1 < nseg:
-            dc.add(seg_start(E, nseg, k + 1) + CMP)
+            dc.add(seg_start(E, nseg, k + 1, warm) + cmpc)
         o, d, _ = decode_range(soft, cr, fl, S, std_init() if k == 0 else np.zeros(64, np.int64),
-                               0 if k == 0 else S + WARM, seg_stop(E, cols, nseg, k), dc)
+                               0 if k == 0 else S + warm, seg_stop(E, cols, nseg, k, warm), dc)
         out.update(o)
         if k:
-            B[k] = d[S + CMP]
+            B[k] = d[S + cmpc]
         if k + 1 < nseg:
-            A[k + 1] = d[seg_start(E, nseg, k + 1) + CMP]
+            A[k + 1] = d[seg_start(E, nseg, k + 1, warm) + cmpc]
     fixes = 0
     bad = [j for j in range(1, nseg) if ((A[j] ^ B[j]) & 0xFE).any()]
     if bad:
@@ -192,15 +195,15 @@ def segmented_decode(soft, cr, fl, nseg):
         # only at a seam past the last disagreeing one whose start state it reproduces
         ks, kl = bad[0], bad[-1]
         fixes = 1
-        S = seg_start(E, nseg, ks) + CMP
-        cmp_cols = {seg_start(E, nseg, j) + CMP: j for j in range(kl + 1, nseg)}
+        S = seg_start(E, nseg, ks, warm) + cmpc
+        cmp_cols = {seg_start(E, nseg, j, warm) + cmpc: j for j in range(kl + 1, nseg)}
 
         def cmp(tr, m):
             j = cmp_cols[tr]
             if not ((m ^ B[j]) & 0xFE).any():
-                return seg_start(E, nseg, j) + WARM + 30
+                return seg_start(E, nseg, j, warm) + warm + 30
             return None
-        o, _, _ = decode_range(soft, cr, fl, S, A[ks], S + WARM - CMP, cols, set(cmp_cols), cmp)
+        o, _, _ = decode_range(soft, cr, fl, S, A[ks], S + warm - cmpc, cols, set(cmp_cols), cmp)
         out.update(o)
     n = max(out) + 1 if out else 0
     return np.array([out[i] for i in range(n)], np.uint8), fixes

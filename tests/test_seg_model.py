@@ -9,21 +9,24 @@ from tests import seg_model as SM
 from tests.golden import synth
 
 
-def test_geometry_invariants():
+@pytest.mark.parametrize("warm", [SM.WARM, SM.WARM_UNI])
+def test_geometry_invariants(warm):
     for fl in list(range(384, 5000, 37)) + [2050, 4095]:
         E = 8 * fl + 6
         for cr in (0, 1, 2):
             K = (24, 32, 36)[cr]                             # decoded bits per 48 soft values
             cols = -(-E // K) * K
             for nseg in range(2, min(SM.MAX_SEG, E // SM.MIN_CUT) + 1):
-                S = [SM.seg_start(E, nseg, k) for k in range(nseg)]
+                S = [SM.seg_start(E, nseg, k, warm) for k in range(nseg)]
                 assert S[0] == 0 and all(b > a for a, b in zip(S, S[1:]))
                 for k in range(1, nseg):
-                    assert S[k] % 768 == 0 and S[k] >= 768
-                    assert S[k] + SM.WARM + 64 <= E          # window J_k - 256 fires before the frame end
-                    assert (S[k] + SM.CMP) % 24 == 0         # the seam column is a body end
+                    J = S[k] + warm                          # first output bit: a window boundary
+                    assert J % 768 == 256 and S[k] % 24 == 0 and S[k] > 0
+                    assert J + 64 <= E                       # window J_k - 256 fires before the frame end
+                    assert (S[k] + warm - 16) % 24 == 0      # the seam column is a body end
+                    assert S[k] + warm - 16 > S[k - 1]       # ... inside segment k - 1
                 for k in range(nseg):
-                    assert SM.seg_stop(E, cols, nseg, k) > S[k] + SM.CMP
+                    assert SM.seg_stop(E, cols, nseg, k, warm) > S[k] + warm - 16
 
 
 def test_row_bound():
@@ -81,33 +84,36 @@ CASES = [(cr, fl, noise, nseg) for cr in (0, 1, 2) for fl, noise, nseg in
           (500, 2, 3), (500, -1, 3)]]      # (500: E / 3 = 1335 >= kMinCut, a one-unit middle segment)
 
 
+@pytest.mark.parametrize("warm", [SM.WARM, SM.WARM_UNI])
 @pytest.mark.parametrize("cr,fl,noise,nseg", CASES)
-def test_segmented_equals_oracle(oracle, cr, fl, noise, nseg):
+def test_segmented_equals_oracle(oracle, cr, fl, noise, nseg, warm):
     s = synth.viterbi_soft(cr, fl, noise, seed=100 * cr + fl + noise)
     exp = oracle.viterbi_decode(s, fl, cr)
-    got, fixes = SM.segmented_decode(s, cr, fl, nseg)
+    got, fixes = SM.segmented_decode(s, cr, fl, nseg, warm)
     assert got.size == exp.size == fl
     assert (got == exp).all()
     if noise >= 0:
         assert fixes == 0                                # clean frames converge in the warm-up
 
 
-def test_pure_noise_exercises_fix(oracle):
+@pytest.mark.parametrize("warm", [SM.WARM, SM.WARM_UNI])
+def test_pure_noise_exercises_fix(oracle, warm):
     """Pure-noise frames: some seam disagrees, the fix row re-decodes from it, still exact."""
     fixes = 0
     for seed in range(6):
         s = synth.viterbi_soft(2, 900, -1, seed=seed)
-        got, f = SM.segmented_decode(s, 2, 900, 4)
+        got, f = SM.segmented_decode(s, 2, 900, 4, warm)
         assert (got == oracle.viterbi_decode(s, 900, 2)).all(), seed
         fixes += f
     assert fixes > 0
 
 
-def test_pure_noise_many_seams(oracle):
+@pytest.mark.parametrize("warm", [SM.WARM, SM.WARM_UNI])
+def test_pure_noise_many_seams(oracle, warm):
     """Long pure-noise frames cut into 8: several seams disagree, not always next to each
     other (a fix row that stopped at the first seam it agrees with would leave a later
     disagreeing segment in place)."""
     for seed in (7041, 41, 42):                          # 7041: seams 1, 4, 6, 7 disagree
         s = synth.viterbi_soft(2, 2035, -1, seed=seed)
-        got, _ = SM.segmented_decode(s, 2, 2035, 8)
+        got, _ = SM.segmented_decode(s, 2, 2035, 8, warm)
         assert (got == oracle.viterbi_decode(s, 2035, 2)).all(), seed

@@ -328,8 +328,20 @@ template <> struct Rate<2> { static constexpr int steps = 3, G = 4, chunk = 32; 
 // the frame's end).  Bit-exact either way; warm-up from zero converges in < 100 columns on
 // every chain input measured, so the fix pass normally finds nothing to do.
 constexpr uint32_t kSegUnit = 768;
-constexpr uint32_t kSegWarm = 256;                     // S_k -> J_k
-constexpr uint32_t kSegCmp = 240;                      // S_k -> C_k
+// Warm-up W = J_k - S_k, and C_k = S_k + W - 16 (the last body end before J_k).  J_k = 768 m_k
+// + 256 whatever W is, so W = 16 mod 24 keeps S_k a multiple of 24.  A uniform batch's rows are
+// placed so that every wave holds one segment index k (viterbi_rows), so its waves' windows
+// stay aligned with any W and it warms up for 136 columns: soft values from the chain converge
+// within 72 columns at AWGN sigma 4..12 and within 120 at sigma 58, where CRCs start to fail
+// (warm-ups from zero at every 768th column of config-3 packets, 420 per sigma, brick loop in
+// numpy), and 120 columns fewer per seam than 256 take 7.5 % off a 2048-packet shard's longest
+// row.  A mixed batch's segments of one packet share a wave with segment 0, whose windows sit at
+// multiples of 256: it keeps W = 256.
+constexpr uint32_t kSegWarm = 256;                     // S_k -> J_k (mixed batches)
+constexpr uint32_t kSegWarmUni = 136;                  // S_k -> J_k (uniform batches)
+static_assert(kSegWarm % 24 == 16 && kSegWarmUni % 24 == 16, "S_k = J_k - W must stay a multiple of 24");
+__host__ __device__ constexpr uint32_t seg_cmp(uint32_t warm) { return warm - 16u; }   // S_k -> C_k
+constexpr uint32_t kSegCmp = seg_cmp(kSegWarm);
 constexpr int kMaxSeg = 8;
 constexpr uint32_t kMinSeg = 1536;                     // columns per segment at least (mixed batch)
 // A uniform batch too small to give every SIMD two waves of whole frames is cut into segments
@@ -401,9 +413,9 @@ constexpr int kPlanUnit = kRows;                       // rows ranked together b
 // start unit m_k of segment k >= 1 of nseg over a frame of E = 8 len + 6 columns (rounded
 // k E / nseg; with E / nseg >= kMinCut the m_k are distinct (steps of > 1 unit) and
 // S_k + 256 + 64 <= E (the last start is at most (nseg - 1) E / nseg + 384))
-__host__ __device__ __forceinline__ uint32_t seg_start(uint32_t E, uint32_t nseg, uint32_t k) {
+__host__ __device__ __forceinline__ uint32_t seg_start(uint32_t E, uint32_t nseg, uint32_t k, uint32_t warm = kSegWarm) {
   // floor(x / (1536 nseg)) = floor(floor(x / 1536) / nseg)
-  return k == 0 ? 0u : kSegUnit * udiv_small((2u * k * E + nseg * kSegUnit) / (2u * kSegUnit), nseg);
+  return k == 0 ? 0u : kSegUnit * udiv_small((2u * k * E + nseg * kSegUnit) / (2u * kSegUnit), nseg) + kSegWarm - warm;
 }
 // segments for a frame of E columns with cols columns of input, target length L, segments of
 // at least min_len (kMinSeg or kMinCut) columns
@@ -415,8 +427,9 @@ __host__ __device__ __forceinline__ uint32_t seg_count(uint32_t E, uint32_t cols
   return min(max(n, 1u), (uint32_t)kMaxSeg);
 }
 // first column after segment k (absolute): where segment k + 1's first window is written
-__host__ __device__ __forceinline__ uint32_t seg_stop(uint32_t E, uint32_t cols, uint32_t nseg, uint32_t k) {
-  return k + 1u < nseg ? seg_start(E, nseg, k + 1u) + kSegWarm + 30u : cols;
+__host__ __device__ __forceinline__ uint32_t seg_stop(uint32_t E, uint32_t cols, uint32_t nseg, uint32_t k,
+                                                      uint32_t warm = kSegWarm) {
+  return k + 1u < nseg ? seg_start(E, nseg, k + 1u, warm) + warm + 30u : cols;
 }
 // dump of seam j (1 <= j < nseg) of packet p, side 0 (segment j - 1) or 1 (segment j)
 __host__ __device__ __forceinline__ size_t seam_index(uint32_t p, uint32_t j, uint32_t side) {
@@ -426,7 +439,7 @@ __host__ __device__ __forceinline__ size_t seam_index(uint32_t p, uint32_t j, ui
 // Cold per-row facts for the seam events, one entry per row of the block (LDS).
 struct RowX {
   uint32_t p;                                          // packet
-  uint32_t kn;                                         // k | nseg << 8 | fix << 16 | matched << 17 | seam j << 20
+  uint32_t kn;                                         // k | nseg << 8 | fix << 16 | matched << 17 | short warm-up << 18 | seam j << 20
   uint32_t S, E;                                       // first column (absolute), 8 len + 6
 };
 
@@ -480,6 +493,7 @@ __device__ __forceinline__ void seam_event(Row& R, uint32_t tr, const uint32_t (
                                         RowX* rowx, uint2* __restrict__ dumps) {
   RowX x = rowx[rib];
   const uint32_t k = x.kn & 0xFFu, nseg = (x.kn >> 8) & 0xFFu, fix = (x.kn >> 16) & 1u, j = x.kn >> 20;
+  const uint32_t W = (x.kn >> 18) & 1u ? kSegWarmUni : kSegWarm;
   (void)tr;
 #ifdef ZRX_GUARD
   if (x.p >= g_zg_np || j == 0 || j >= nseg || nseg > (uint32_t)kMaxSeg) {
@@ -494,7 +508,7 @@ __device__ __forceinline__ void seam_event(Row& R, uint32_t tr, const uint32_t (
     dump_store(dumps + seam_index(x.p, j, side), l, M);
     if (side == 1u && k + 1u < nseg) {
       x.kn = (x.kn & 0xFFFFFu) | ((k + 1u) << 20);
-      R.evc = seg_start(x.E, nseg, k + 1u) + kSegCmp - x.S;
+      R.evc = seg_start(x.E, nseg, k + 1u, W) + seg_cmp(W) - x.S;
     } else {
       R.evc = kNever;
     }
@@ -506,12 +520,12 @@ __device__ __forceinline__ void seam_event(Row& R, uint32_t tr, const uint32_t (
     for (int i = 0; i < kDw; i++) d |= M[i] ^ B[i];
     const uint64_t bad = __builtin_amdgcn_ballot_w64((d & 0x7F007F00u) != 0u);
     if (row_bits(bad) == 0u) {                         // the row's 64 H bytes agree
-      R.cols = min(R.cols, seg_start(x.E, nseg, j) + kSegWarm + 30u - x.S);
+      R.cols = min(R.cols, seg_start(x.E, nseg, j, W) + W + 30u - x.S);
       x.kn |= 1u << 17;
       R.evc = kNever;
     } else if (j + 1u < nseg) {
       x.kn = (x.kn & 0xFFFFFu) | ((j + 1u) << 20);
-      R.evc = seg_start(x.E, nseg, j + 1u) + kSegCmp - x.S;
+      R.evc = seg_start(x.E, nseg, j + 1u, W) + seg_cmp(W) - x.S;
     } else {
       R.evc = kNever;
     }
@@ -1257,9 +1271,13 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
     int p = slot;
     uint32_t k = 0, nseg = 1;
     if (valid && rows) {
-      if (uni) {                                       // a uniform batch: row r = segment r mod u of packet r / u
+      if (uni) {
+        // a uniform batch: row r = segment r / np of packet r mod np (np = nrows / u), so a
+        // wave's rows are one segment index of consecutive packets: their windows line up
+        // (the deferred walk is per wave) whatever the warm-up
         const uint32_t r = v3::order_place((uint32_t)slot, (uint32_t)nrows / v3::kRows, ncu, ncu_rcp);
-        p = (int)v3::udiv_small(r, uni); k = r - (uint32_t)p * uni; nseg = uni;
+        const uint32_t np = (uint32_t)nrows / uni;
+        k = r / np; p = (int)(r - k * np); nseg = uni;
       } else {
         const int2 r = rows[slot];
         p = r.x; k = (uint32_t)r.y & 0xFFu; nseg = ((uint32_t)r.y >> 8) & 0xFFu;
@@ -1287,6 +1305,7 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
       fl = vp[0]; cr = vp[1]; n = vp[2];
       so = soft_off[p]; oo = out_off[p];
     }
+    const uint32_t W = uni ? v3::kSegWarmUni : v3::kSegWarm;   // warm-up of the segments
     const uint32_t cols = load && n > 0 && cr >= 0 && cr <= 2 ? (uint32_t)(n / (cr == 0 ? 2 : cr == 1 ? 3 : 4)) * (uint32_t)(cr + 1) : 0u;
     const uint32_t E = (uint32_t)fl * 8u + 6u;
     // this row's segment: first column S, last column, seam j of its first seam event
@@ -1307,7 +1326,7 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
         }
       }
       work = work && ks != 0u;
-      if (work) { S = v3::seg_start(E, nseg, ks) + v3::kSegCmp; j = kl + 1u; k = ks; }
+      if (work) { S = v3::seg_start(E, nseg, ks, W) + v3::seg_cmp(W); j = kl + 1u; k = ks; }
 #ifdef ZRX_GUARD
       if (work && l == 0)
         printf("ZG fix row: blk %d rib %u p %d nseg %u ks %u S %u E %u cols %u cr %d n %d\n", (int)blockIdx.x, rib, p, nseg,
@@ -1315,13 +1334,14 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
 #endif
       if (work && l == 0 && stats) atomicAdd(stats + 1, 1);
     } else if (nseg > 1u && work) {
-      S = v3::seg_start(E, nseg, k);
-      stop = v3::seg_stop(E, cols, nseg, k);
+      S = v3::seg_start(E, nseg, k, W);
+      stop = v3::seg_stop(E, cols, nseg, k, W);
       j = k ? k : 1u;
     }
     // (cold facts in LDS: read back where needed instead of held in registers by the decode)
     // (fix rows: k holds ks, the seam they start at)
-    rowx[rib] = v3::RowX{(uint32_t)p, k | (nseg << 8) | ((uint32_t)(fix != 0) << 16) | (j << 20), S, E};
+    rowx[rib] = v3::RowX{(uint32_t)p, k | (nseg << 8) | ((uint32_t)(fix != 0) << 16) | ((uint32_t)(uni != 0u) << 18) | (j << 20),
+                         S, E};
     const int64_t sS = work ? (int64_t)(S / (uint32_t)(cr + 1)) * (cr == 0 ? 2 : cr == 1 ? 3 : 4) : 0;   // soft values before S
     so += sS;
     const uint32_t nS = work ? (uint32_t)((int64_t)n - sS) : 0u;
@@ -1350,6 +1370,7 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
         const v3::RowX x = rowx[rib];
         const uint32_t xk = x.kn & 0xFFu, xn = (x.kn >> 8) & 0xFFu, xj = x.kn >> 20;
         const bool xfix = (x.kn >> 16) & 1u;
+        const uint32_t xw = (x.kn >> 18) & 1u ? v3::kSegWarmUni : v3::kSegWarm;
         uint32_t M[v3::kDw];
         if (xfix && mq) {                               // segment ks - 1's exact state at S = C_ks
           v3::dump_load(dumps + v3::seam_index(x.p, x.kn & 0xFFu, 0), l, M);
@@ -1367,9 +1388,9 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
         const bool lrpt = !FIX && (v3::kPrioMode == 2 || (v3::kPrioMode == 3 && mixed));
         const bool younger = !FIX && (v3::kPrioMode == 1 || (v3::kPrioMode == 3 && !mixed)) && ((blockIdx.x / ncu) & 1u) != 0u;
         v3::Row Rr;
-        Rr.ob = xfix ? v3::kSegWarm - v3::kSegCmp : xk ? v3::kSegWarm : 0u;
+        Rr.ob = xfix ? xw - v3::seg_cmp(xw) : xk ? xw : 0u;
         Rr.end = x.E - x.S; Rr.cols = colsS;
-        Rr.evc = xj != 0u && xj < xn ? v3::seg_start(x.E, xn, xj) + v3::kSegCmp - x.S : v3::kNever;
+        Rr.evc = xj != 0u && xj < xn ? v3::seg_start(x.E, xn, xj, xw) + v3::seg_cmp(xw) - x.S : v3::kNever;
         Rr.live = mq;
         Rr.ppend = Rr.fpend = false;
         Rr.pT = Rr.plook = Rr.fT = Rr.fcnt = Rr.flook = 0;
