@@ -79,8 +79,8 @@ def main():
                          "turn, as a streaming receiver would, so one batch's tail overlaps the next one's head; "
                          "0 (default) = auto: 2 for an rx batch under %d packets per GPU (zrx_pipeline_link "
                          "mode 1) and for configs 2 and 5, else 1" % PIPELINE_BELOW)
-    ap.add_argument("--link", type=int, default=-1, choices=[-1, 0, 1, 2, 3, 4, 5, 6, 7],
-                    help="zrx_pipeline_link mode of two engines (-1: auto = 1 for configs 3/4, 4 for config 5)")
+    ap.add_argument("--link", type=int, default=-1, choices=list(range(-1, 16)),
+                    help="zrx_pipeline_link mode of two engines (-1: auto = 9 for configs 3/4, 4 for config 5)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="with --gpus N: every rank on GPU 0 over a gloo process group (the multi-rank path on a "
                          "one-GPU box; functional, not a scaling point)")
@@ -198,12 +198,12 @@ def rx_run(args, total, world, rank, local, dev):
     npipe = args.pipeline or (2 if hi - lo < PIPELINE_BELOW else 1)
     # npipe engines, each with its own workspace and stream, take the steps in turn; every
     # step is still one whole pass of the chain over one batch.  Two engines are linked
-    # (zrx_pipeline_link mode 1): one batch's Viterbi starts only once the other batch's chain
-    # is done, so only the short kernels around it overlap.
+    # (zrx_pipeline_link mode 9): one batch's Viterbi starts only once the other batch's
+    # Viterbi and seam pass are done, so only the short kernels around it overlap.
     engs = [RxEngine(local) for _ in range(npipe)]
     streams = [torch.cuda.Stream(dev) for _ in range(npipe)]
     if npipe == 2 and args.link != 0:
-        engs[0].link(engs[1], 1 if args.link < 0 else args.link)
+        engs[0].link(engs[1], 9 if args.link < 0 else args.link)
     eng = engs[0]
     state = {}
 
@@ -303,7 +303,7 @@ def rx_run(args, total, world, rank, local, dev):
                    "batches_per_gpu": nb,
                    "pipeline": f"{len(engs)} batch{'es' if len(engs) > 1 else ''} in flight"
                                + (" (engines on separate streams, steps in turn, linked: a Viterbi starts after "
-                                  "the other batch's chain)" if len(engs) > 1 else "")},
+                                  "the other batch's Viterbi)" if len(engs) > 1 else "")},
         "value_one_engine": round(res["bits"] * args.steps / single / 1e6, 1),
         "stage_ms": {k: round(v, 4) for k, v in stage.items()},
         "roofline": {"kernel": "k_viterbi3 (data Viterbi)", "bound": "valu",

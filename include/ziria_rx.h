@@ -176,8 +176,9 @@ int zrx_get_timing(zrx_ctx* ctx, float* ms5);
  * otherwise idle GPU); with bit 1 its data FFT waits until the peer's last launched data
  * Viterbi has finished; with bit 2 its chain's head (SIGNAL, plan, data FFT) runs on a
  * lowest-priority stream of its own, forked from and joined back into the context's stream,
- * so the peer's Viterbi blocks are dispatched ahead of it.  Event waits and stream choice
- * only: results never change. */
+ * so the peer's Viterbi blocks are dispatched ahead of it; with bits 0 and 3 the data Viterbi
+ * waits only for the peer's last data Viterbi and seam pass (the peer's descramble/CRC then
+ * overlaps it).  Event waits and stream choice only: results never change. */
 int zrx_pipeline_link(zrx_ctx* a, zrx_ctx* b, int mode);
 
 /* d_in/d_out: 64*nsym complex16 each (may alias). */

@@ -141,7 +141,7 @@ def test_bench_pipelined_flow(oracle, tmp_path, args, k, w):
     verify = rest[k:k + 2 * nb]
     assert [e[1:] for e in verify] == [[j, bi] for bi in range(nb) for j in range(2)]
     if "--config" not in args:                      # config 3: the single-engine pass, K steps on engine 0
-        assert ["link", 0, 1, 1] in log and ["plan_check", 0] in log and ["plan_check", 1] in log
+        assert ["link", 0, 1, 9] in log and ["plan_check", 0] in log and ["plan_check", 1] in log
         single = rest[k + 2 * nb:]                  # its own warmup, then the K timed steps
         assert [e[1:] for e in single] == [[0, i % nb] for i in range(w)] + [[0, i % nb] for i in range(k)]
         assert line["config"]["batches_per_gpu"] == nb and b["packets"] == nb * 24

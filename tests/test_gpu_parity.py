@@ -438,7 +438,7 @@ def test_chain_plan_reuse(engine):
         check(x, nsym, pay, info, bad)
 
 
-@pytest.mark.parametrize("mode", [1, 2, 4, 5, 6, 7])
+@pytest.mark.parametrize("mode", [1, 2, 4, 5, 6, 7, 9, 13])
 def test_chain_linked_engines(mode):
     """Two engines linked (zrx_pipeline_link bits: 1 the Viterbi waits for the peer's chain,
     2 the data FFT waits for the peer's Viterbi, 4 the chain's head on a lowest-priority stream

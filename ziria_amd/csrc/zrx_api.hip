@@ -487,7 +487,7 @@ int zrx_set_stream(zrx_ctx* c, void* stream) {
 }
 
 int zrx_pipeline_link(zrx_ctx* a, zrx_ctx* b, int mode) {
-  if (!a || !b || a == b || mode < 0 || mode > 7) return ZRX_EINVAL;
+  if (!a || !b || a == b || mode < 0 || mode > 15) return ZRX_EINVAL;
   // the link orders two streams of one device (events without a system fence, the low-
   // priority head stream beside the engine's own): both engines must be on it
   if (a->device != b->device) return ZRX_EINVAL;
@@ -712,10 +712,7 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
     *(volatile int32_t*)c->mixed_hint = 0;
   }
   const bool split = ordered && *(volatile int32_t*)c->mixed_hint != 0;
-  k_pkt_plan<<<1, 1024, 0, h>>>(c->vparams, npkts, c->soft_off, c->dsym, c->wave_p0, ordered ? c->rows : nullptr,
-                                c->nrows, c->segs, c->order, c->dec_bits, c->ncu, (int)plan_rows_max(c, npkts),
-                                split ? 1 : 0, ordered ? c->mixed_hint_dev : nullptr);
-  if (split) {
+  if (split) {                                         // forked before the plan: see k_pkt_rows
     if (!c->side) {
       ZRX_CHECK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
       // (stream-to-stream on one device: no system-scope fence, which writes back the L2s)
@@ -728,6 +725,9 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
                                         (int)plan_rows_max(c, npkts));
     ZRX_CHECK(hipEventRecord(c->ev_join, c->side));
   }
+  k_pkt_plan<<<1, 1024, 0, h>>>(c->vparams, npkts, c->soft_off, c->dsym, c->wave_p0, ordered ? c->rows : nullptr,
+                                c->nrows, c->segs, c->order, c->dec_bits, c->ncu, (int)plan_rows_max(c, npkts),
+                                split ? 1 : 0, ordered ? c->mixed_hint_dev : nullptr);
   if (ev) ZRX_CHECK(hipEventRecord(ev[2], h));
   // k_data_fft: waves over the batch's data symbols, at most npkts x (max_nsym - 1) of them
   const int fft_blocks = (int)std::min<int64_t>(((int64_t)npkts * (max_nsym - 1) + 255) / 256,
@@ -749,7 +749,10 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
     ZRX_CHECK(hipEventRecord(c->ev_lo_join, h));
     ZRX_CHECK(hipStreamWaitEvent(s, c->ev_lo_join, 0));
   }
-  if (peer && (c->link_mode & 1)) ZRX_CHECK(hipStreamWaitEvent(s, peer->ev_chain_done, 0));
+  // (mode bit 3: only for the peer's Viterbi and seam pass, so its descramble/CRC overlaps the
+  // start of this Viterbi)
+  if (peer && (c->link_mode & 1))
+    ZRX_CHECK(hipStreamWaitEvent(s, (c->link_mode & 8) ? peer->ev_vit_done : peer->ev_chain_done, 0));
   launch_viterbi(c, c->soft, c->soft_off, c->vparams, npkts, c->dec, c->dec_off, c->dec_bits, ordered);
   if (peer) ZRX_CHECK(hipEventRecord(c->ev_vit_done, s));
   if (ev) ZRX_CHECK(hipEventRecord(ev[4], s));

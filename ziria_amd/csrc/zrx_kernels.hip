@@ -538,26 +538,49 @@ __global__ __launch_bounds__(1024) void k_pkt_plan(const int32_t* __restrict__ v
     return;
   }
   if (split) {                                         // k_pkt_rows sorts and expands, on a side stream
-    if (t == 0) { nrows[v3::kPlanUniform] = 0; nrows[v3::kPlanSegLen] = (int32_t)Lm; }
+    if (t == 0) nrows[v3::kPlanUniform] = 0;            // (k_pkt_rows writes the same)
     return;
   }
   plan_rows_mixed(vparams, npkts, Lm, rows, nrows, segs, order, out_bits, ncu, rows_cap, hist, &rtotal);
 }
 
 // The second half of a split plan (rx chain): the mixed batch's sort and row expansion, on a
-// side stream while k_data_fft runs (it needs only the first half's offsets).  Nothing to do
-// for a uniform batch, whose header k_pkt_plan wrote.
+// side stream forked right after k_signal_vit, so it runs beside k_pkt_plan and k_data_fft
+// (one block of 1024 threads: config 5's takes ~140 us, longer than k_data_fft alone).  It
+// needs only the packets' parameters: the batch's column total (for the segment length) and
+// whether it is uniform are recounted here exactly as k_pkt_plan counts them (one more read of
+// 16 B per packet), so the two kernels share no state but the header words they both write
+// with equal values.  Nothing to do for a uniform batch: k_pkt_plan writes its header.
 __global__ __launch_bounds__(1024) void k_pkt_rows(const int32_t* __restrict__ vparams, int npkts,
                                                    int2* __restrict__ rows, int32_t* __restrict__ nrows,
                                                    uint8_t* __restrict__ segs, int32_t* __restrict__ order,
                                                    int32_t* __restrict__ out_bits, int ncu, int rows_cap) {
-  if (nrows[v3::kPlanUniform] != 0) return;
   __shared__ uint32_t hist[kOrderPerThread * 1024];
-  __shared__ uint32_t rtotal;
-  const uint32_t Lm = (uint32_t)nrows[v3::kPlanSegLen];
-  for (int i = threadIdx.x; i < kOrderPerThread * 1024; i += 1024) hist[i] = 0;
-  if (threadIdx.x == 0) rtotal = 0;
+  __shared__ uint32_t rtotal, uniform;
+  __shared__ unsigned long long tcols;
+  const int t = threadIdx.x;
+  if (t == 0) { rtotal = 0; uniform = 1; tcols = 0; }
+  for (int i = t; i < kOrderPerThread * 1024; i += 1024) hist[i] = 0;
   __syncthreads();
+  // (k_pkt_plan's rule: every packet asks for packet 0's {frame_len, rate, soft_len,
+  // modulation} and it has trellis columns)
+  const int4 q0 = npkts > 0 ? *reinterpret_cast<const int4*>(vparams) : make_int4(0, 0, 0, 0);
+  bool same = cols_of(q0.y, q0.z) > 0;
+  uint64_t my_cols = 0;
+  for (int p = t; p < npkts; p += 1024) {
+    const int4 q = *reinterpret_cast<const int4*>(vparams + 4 * (int64_t)p);
+    my_cols += cols_of(q.y, q.z);
+    same = same && q.x == q0.x && q.y == q0.y && q.z == q0.z && q.w == q0.w;
+  }
+  for (int o = 32; o > 0; o >>= 1) my_cols += (uint64_t)__shfl_xor((long long)my_cols, o);
+  if ((t & 63) == 0) atomicAdd(&tcols, (unsigned long long)my_cols);
+  if (!same) uniform = 0;
+  __syncthreads();
+  if (uniform) return;
+  const uint64_t rt = 64ull * (uint64_t)max(ncu, 1);   // (k_pkt_plan's segment length Lm)
+  const uint32_t L0 = (uint32_t)min<uint64_t>((tcols + rt - 1) / rt, 0xFFFFFFFFull);
+  const uint32_t L = max(L0, v3::kMinSeg);
+  const uint32_t Lm = max(L * v3::kSegMixNum / 8u, v3::kMinSeg);
   plan_rows_mixed(vparams, npkts, Lm, rows, nrows, segs, order, out_bits, ncu, rows_cap, hist, &rtotal);
 }
 
