@@ -600,13 +600,6 @@ constexpr int kDfLutCopies = 4;       // demap LUT copies (lane & 3): fewer LDS 
 
 __device__ __forceinline__ int soft_units_of(int mod) { return mod == 0 ? 3 : mod == 1 ? 6 : mod == 2 ? 12 : 18; }
 
-template <int MOD, bool EQ, class St>
-__device__ __forceinline__ void data_fft_symbol(s2* x, int k, const uint32_t* lut, St st,
-                                                const uint32_t* __restrict__ cp, const EqTabs& T) {
-  fft64_inplace(x);
-  if constexpr (EQ) equalize_data_bins(x, [cp](int b) { return as_s2(cp[b]); }, k + 1, T);
-  demap_deinterleave_st<MOD>(x, [lut](uint32_t i) { return lut[i * kDfLutCopies]; }, st);
-}
 
 // This lane's symbol of wave w: packet, index in the packet, modulation, symbol index, soft row.
 struct DfSym {
@@ -703,13 +696,19 @@ __global__ __launch_bounds__(256) void k_data_fft(const uint4* __restrict__ sym,
     // ---- compute
     const uint32_t* cp = EQ ? chan + (int64_t)d.p * 64 : nullptr;
     if (d.valid) {
+      // the FFT (and EQ) for every lane at once, then the demapper of the lane's modulation:
+      // with the FFT inside the per-modulation branches a wave whose symbols mix modulations
+      // (config 5) ran it once per modulation present
+      fft64_inplace(x);
+      if constexpr (EQ) equalize_data_bins(x, [cp](int b) { return as_s2(cp[b]); }, d.k + 1, T);
       uint4* row = stage + kDfRow * lane;
       auto st = [row](int q, uint4 v) { row[q] = v; };
+      auto lu = [lut](uint32_t i) { return lut[i * kDfLutCopies]; };
       switch (d.mod) {
-        case 0: data_fft_symbol<0, EQ>(x, d.k, lut, st, cp, T); break;
-        case 1: data_fft_symbol<1, EQ>(x, d.k, lut, st, cp, T); break;
-        case 2: data_fft_symbol<2, EQ>(x, d.k, lut, st, cp, T); break;
-        default: data_fft_symbol<3, EQ>(x, d.k, lut, st, cp, T); break;
+        case 0: demap_deinterleave_st<0>(x, lu, st); break;
+        case 1: demap_deinterleave_st<1>(x, lu, st); break;
+        case 2: demap_deinterleave_st<2>(x, lu, st); break;
+        default: demap_deinterleave_st<3>(x, lu, st); break;
       }
     }
     __builtin_amdgcn_wave_barrier();
