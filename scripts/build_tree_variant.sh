@@ -18,5 +18,8 @@ assert old in s, "old text not found"
 open(p, "w").write(s.replace(old, new))
 PY
 cd "$TMP/ziria_amd/csrc"
-hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DZRX_EXPERIMENTS -o "$ROOT/ziria_amd/_lib/libziria_rx.$NAME.so" zrx_api.hip
+python3 gen_tables.py
+for f in zrx_host zrx_ext_cxx; do g++ -O3 -std=c++17 -fPIC -c $f.cpp -o "$TMP/$f.o"; done
+hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -pthread -DZRX_EXPERIMENTS -o "$ROOT/ziria_amd/_lib/libziria_rx.$NAME.so" \
+  zrx_api.hip -x none "$TMP/zrx_host.o" "$TMP/zrx_ext_cxx.o"
 echo "$ROOT/ziria_amd/_lib/libziria_rx.$NAME.so"

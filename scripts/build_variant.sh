@@ -16,6 +16,6 @@ for f in zrx_host zrx_ext_cxx; do
     OBJS="$OBJS $TMP/$f.o"
   fi
 done
-hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DZRX_EXPERIMENTS $FLAGS -o "$ROOT/ziria_amd/_lib/libziria_rx.$NAME.so" \
+hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -pthread -DZRX_EXPERIMENTS $FLAGS -o "$ROOT/ziria_amd/_lib/libziria_rx.$NAME.so" \
   "$TMP/ziria_amd/csrc/zrx_api.hip" ${OBJS:+-x none $OBJS}
 echo "$ROOT/ziria_amd/_lib/libziria_rx.$NAME.so"

@@ -1245,7 +1245,7 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
 //          re-decodes from the first seam whose two dumps disagree (usually none).
 // The grid may be smaller than the rows (block-stride loop).
 #ifdef ZRX_VTRACE
-// (timeline probe builds only: scripts/exp/vit_trace.py) 8 words per row slot: start and end
+// (timeline probe builds only: scripts/exp/vit_trace.py, in git history at e0a0913) 8 words per row slot: start and end
 // (s_memrealtime, 100 MHz, low words), HW_ID, XCC_ID, block, columns, rate, packet
 __device__ uint32_t* g_vtrace;
 __device__ uint32_t g_vtrace_rows;                     // row slots the buffer holds
