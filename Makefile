@@ -29,7 +29,7 @@ $(ASAN_DIR)/libziria_rx.so: $(CSRC)
 	mkdir -p $(ASAN_DIR)
 	for f in zrx_host zrx_ext_cxx; do $(CLANG) -O1 -g -std=c++17 -fPIC -fsanitize=address,undefined \
 	  -fno-omit-frame-pointer -c ziria_amd/csrc/$$f.cpp -o $(ASAN_DIR)/$$f.o || exit 1; done
-	cd ziria_amd/csrc && hipcc --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -shared -Wall $(HOST_SAN) \
+	cd ziria_amd/csrc && hipcc --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -shared -pthread -Wall $(HOST_SAN) \
 	  -o ../_lib/asan/libziria_rx.so zrx_api.hip -x none ../_lib/asan/zrx_host.o ../_lib/asan/zrx_ext_cxx.o
 
 $(ASAN_DIR)/ziria_rx_driver: tools/ziria_rx_driver.cpp integration/csrc/hip_ext_batch.cpp $(ASAN_DIR)/libziria_rx.so
