@@ -110,3 +110,28 @@ def test_viterbi_batch_decode_keeps_caller_bytes(pinned):
     assert (_np(out) == d_out.cpu().numpy()).all()
     b = bits.cpu().numpy()
     assert (b[::7] < 8 * 1500).all() and (b[1::7] == 8 * 1500).all()
+
+
+def test_wifi_rx_eq_batch_chunked():
+    """The EQ external (ChannelEqualization + PilotTrack) through the same pipeline: 4600
+    packets through a channel (three chunks, the channel coefficients uploaded with their
+    chunk's symbols), pageable arrays, against the device API."""
+    b = txgen.make_batch(4600, seed=0x52, sigma=2.0, device="cuda", channel=True)
+    n, S = 4600, b["max_nsym"]
+    e = RxEngine(0)
+    e.reserve(n, S)
+    pay_d, info_d = e.rx(b["sym"], b["sym_off"], b["nsym"], S, chan=b["chan"])
+    torch.cuda.synchronize()
+    e.close()
+    pay_d, info_d = pay_d.cpu().numpy(), info_d.cpu().numpy()
+    sym = np.ascontiguousarray(b["sym"].cpu().numpy())
+    chan = np.ascontiguousarray(b["chan"].cpu().numpy())
+    csr = (np.arange(n + 1) * S).astype(np.int32)
+    pay = np.zeros((n, 4096), np.uint8)
+    info = np.zeros((n, 8), np.int32)
+    rc = lib().__ext_wifi_rx_eq_batch(_p(sym), sym.shape[0], _p(csr), n + 1, _p(chan), n * 64, _p(pay), n * 4096 * 8,
+                                      _p(info), n * 8)
+    assert rc == int((info_d[:, 4] == 1).sum()) > n - 50
+    assert (info == info_d).all()
+    ok = info[:, 4] == 1
+    assert (pay[ok, :1500] == pay_d[ok, :1500]).all() and (pay[ok, :1500] == b["payload"][ok]).all()
