@@ -129,8 +129,11 @@ def test_bench_pipelined_flow(oracle, tmp_path, args, k, w):
     on = rx.index(["timing", True])
     off = rx.index(["timing", False])
     warm, inst, rest = rx[:on], rx[on + 1:off], rx[off + 1:]
+    settle = warm[w:]                               # untimed launches on engine 0 before the timers (clock ramp)
+    warm = warm[:w]
     assert [e[1:] for e in warm] == [[i % 2, i % nb] for i in range(w)]
     assert len(inst) >= 3 * nb and all(e[1] == 0 for e in inst) and sorted({e[2] for e in inst}) == [0, 1]
+    assert [e[1:] for e in settle] == [[0, i % nb] for i in range(len(inst))]
     timed = rest[:k]
     assert [e[1:] for e in timed] == [[(w + i) % 2, (w + i) % nb] for i in range(k)]
     if "--config" in args:                          # config 5: engine 0 alone over the timed batches, then the checks
