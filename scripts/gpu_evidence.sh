@@ -23,7 +23,7 @@ for n in 2048 4096 8192; do
   timeout -k 10 300 python bench.py --npkts $n --steps 40 --warmup 5 --no-cpu > gpurun_out/bench_n$n.log 2>&1 || { tail -5 gpurun_out/bench_n$n.log; exit 1; }
   tail -1 gpurun_out/bench_n$n.log | cut -c1-120
 done
-for a in "--config 1" "--config 2 --steps 20" "--config 5 --steps 20" "--config 5 --steps 40" "--eq" "--tx" "--e2e"; do
+for a in "--config 1 --warmup 15" "--config 2 --steps 20 --warmup 15" "--config 5 --steps 20 --warmup 15" "--config 5 --steps 40 --warmup 15" "--eq" "--tx --warmup 15" "--e2e"; do
   step "$a"
   f=gpurun_out/bench_$(echo $a | tr -d ' -').log
   timeout -k 10 300 python bench.py --steps 10 $a > $f 2>&1 || { echo "bench $a failed"; tail -5 $f; exit 1; }

@@ -15,6 +15,7 @@ import glob
 import json
 import os
 import re
+import statistics
 import sys
 from collections import defaultdict
 
@@ -35,16 +36,23 @@ def short(name):
 
 def read_pmc(d):
     per = defaultdict(lambda: defaultdict(float))          # (kernel, dispatch) -> counter -> value
+    durs = {}                                              # (kernel, dispatch) -> ns
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             k = short(r.get("Kernel_Name", ""))
-            per[(k, r.get("Dispatch_Id", "0"))][r["Counter_Name"]] += float(r["Counter_Value"])
+            key = (k, r.get("Dispatch_Id", "0"))
+            per[key][r["Counter_Name"]] += float(r["Counter_Value"])
+            if r.get("Start_Timestamp") and r.get("End_Timestamp"):
+                durs[key] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     out = defaultdict(lambda: defaultdict(list))
-    for (k, _), cs in per.items():
+    clk = defaultdict(list)                                # the shader clock of each dispatch, from its own
+    for key, cs in per.items():                            # GRBM_GUI_ACTIVE and duration (8 XCDs)
         for c, v in cs.items():
-            out[k][c].append(v)
+            out[key[0]][c].append(v)
+        if "GRBM_GUI_ACTIVE" in cs and durs.get(key):
+            clk[key[0]].append(cs["GRBM_GUI_ACTIVE"] / 8 / durs[key])
     return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in out.items()}, \
-           {k: max(len(v) for v in cs.values()) for k, cs in out.items()}
+           {k: max(len(v) for v in cs.values()) for k, cs in out.items()}, clk
 
 
 def read_trace(d):
@@ -52,18 +60,25 @@ def read_trace(d):
     for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             t[short(r["Kernel_Name"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-    return {k: sum(v) / len(v) for k, v in t.items()}
+    return t
 
 
 def main(root):
-    counters, n = {}, {}
+    counters, n, clocks = {}, {}, defaultdict(list)
     for p in sorted(glob.glob(os.path.join(root, "pmc*"))):
         if os.path.isdir(p):
-            c, nn = read_pmc(p)
+            c, nn, ck = read_pmc(p)
             for k, v in c.items():
                 counters.setdefault(k, {}).update(v)
                 n[k] = max(n.get(k, 0), nn[k])
-    dur = read_trace(os.path.join(root, "prof"))
+            for k, v in ck.items():
+                clocks[k] += v
+    trace = read_trace(os.path.join(root, "prof"))
+    # The shader clock climbs from ~2.2 to 2.4 GHz over the first ~10 ms of load after an idle
+    # GPU (profiles/r05/clock_probe.txt), so the trace's first launches run slower: the rates
+    # below use the median launch (the steady clock the bench's timed steps run at); the mean
+    # over every launch is kept beside it.
+    dur = {k: statistics.median(v) for k, v in trace.items()}
     npkts = None
     for lg in glob.glob(os.path.join(root, "pmc*.log")):
         for line in open(lg):
@@ -78,8 +93,8 @@ def main(root):
     except (OSError, subprocess.CalledProcessError):
         rev = None
     res = {"npkts": npkts, "csrc_sha256": source_hash(), "git_head": rev,
-           "source": "rocprofv3 --pmc, one timed step + one warmup of bench.py; "
-                     "durations from the kernel-trace run of the default bench",
+           "source": "rocprofv3 --pmc, one timed step + one warmup of bench.py; durations from the "
+                     "kernel-trace run of the default bench (rates use the median launch)",
            "kernels": {}}
     for k, cs in counters.items():
         if not k.startswith("k_"):
@@ -92,13 +107,17 @@ def main(root):
             e["write_bytes"] = write * 1024
             e["hbm_bytes_per_launch"] = int(e["fetch_bytes_corrected"] + e["write_bytes"])
         if k in dur:
-            e["avg_duration_ns"] = round(dur[k], 1)
+            e["avg_duration_ns"] = round(sum(trace[k]) / len(trace[k]), 1)
+            e["median_duration_ns"] = round(dur[k], 1)
+            e["trace_launches"] = len(trace[k])
             if "SQ_INSTS_VALU" in cs:
                 lane_ops = cs["SQ_INSTS_VALU"] * 64
                 e["valu_lane_ops_per_s"] = lane_ops / (dur[k] * 1e-9)
                 e["valu_issue_frac_of_peak"] = round(e["valu_lane_ops_per_s"] / VALU_PEAK_LANE_OPS, 4)
             if "GRBM_GUI_ACTIVE" in cs:
-                e["effective_clock_ghz"] = round(cs["GRBM_GUI_ACTIVE"] / 8 / dur[k], 3)
+                if clocks.get(k):                      # per dispatch of the PMC pass (its own durations)
+                    e["effective_clock_ghz"] = round(statistics.mean(clocks[k]), 3)
+                    e["effective_clock_ghz_range"] = [round(min(clocks[k]), 3), round(max(clocks[k]), 3)]
                 if "SQ_ACTIVE_INST_VALU" in cs:
                     # gfx94x VALUBusy: SQ_ACTIVE_INST_VALU (quad-cycles) x 4 / SIMDs / GUI cycles
                     e["valu_busy"] = round(cs["SQ_ACTIVE_INST_VALU"] * 4 / 1024 / (cs["GRBM_GUI_ACTIVE"] / 8), 4)
