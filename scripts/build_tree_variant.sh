@@ -1,6 +1,7 @@
 #!/bin/bash
 # Builds the working tree's engine with one text substitution applied (A/B of an uncommitted
 # change): scripts/build_tree_variant.sh NAME FILE OLD_TEXT_FILE NEW_TEXT_FILE
+# (OLD_TEXT_FILE "-": NEW_TEXT_FILE replaces the whole of FILE)
 # -> ziria_amd/_lib/libziria_rx.NAME.so (ZRX_EXPERIMENTS build, as build_variant.sh).
 set -euo pipefail
 NAME=$1; FILE=$2; OLD=$3; NEW=$4
@@ -13,9 +14,14 @@ cp "$ROOT/include/ziria_rx.h" "$TMP/include/"
 python3 - "$TMP/ziria_amd/csrc/$FILE" "$OLD" "$NEW" <<'PY'
 import sys
 p, o, n = sys.argv[1:]
-s = open(p).read(); old = open(o).read(); new = open(n).read()
-assert old in s, "old text not found"
-open(p, "w").write(s.replace(old, new))
+s = open(p).read(); new = open(n).read()
+if o == "-":
+    s = new
+else:
+    old = open(o).read()
+    assert old in s, "old text not found"
+    s = s.replace(old, new)
+open(p, "w").write(s)
 PY
 cd "$TMP/ziria_amd/csrc"
 python3 gen_tables.py
