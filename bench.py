@@ -135,8 +135,8 @@ def main():
     if world > 1 and not args.total:
         strong = rx_run(args, args.npkts, world, rank, local, dev)
 
-    cpu = None
-    if rank == 0 and not args.no_cpu:
+    cpu = None                                         # (the CPU baseline: rank 0 of an N = 1 run only)
+    if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(head["batch0"], args.cpu_seconds, head["batch0"].get("chan"))
 
     if rank == 0:
@@ -168,6 +168,7 @@ def main():
         }
         if world > 1:
             line["ranks"] = world
+            line["cpu_baseline_note"] = "timed at N = 1 only: see the one-GPU line"
         if args.share_gpu:
             line["multi_rank_mode"] = (f"functional: {world} ranks share GPU 0, process group over gloo (host "
                                        "copies); the ranks contend for one GPU, so this is no scaling point")
