@@ -166,7 +166,7 @@ __host__ __device__ constexpr uint32_t snap_delta(int k, int d, int h) {
 // a wrap of the reference's u8 metric (H + BM > 255) sets bit 15, which the guarded column
 // (G) clears after each add ("Guard-free columns": it never happens in the others).  A
 // snapshot byte is bits 7..0 of a half as they are.
-template <int PH, int KPH, int D>
+template <int PH, int KPH, int D, bool BYN = true>
 __device__ __forceinline__ void column_bx(uint32_t (&BX)[kDw], uint32_t (&BY)[kDw], uint32_t P, const Consts& K,
                                           uint32_t C) {
   constexpr uint32_t mk = 1u << KPH;
@@ -176,11 +176,12 @@ __device__ __forceinline__ void column_bx(uint32_t (&BX)[kDw], uint32_t (&BY)[kD
     BX[D] = __builtin_amdgcn_perm(mk * 0x01010101u, P, K.sel[PH][D]);
   } else if constexpr ((src >> 8) == 0) {
     BX[D] = BX[src & 0xFF];
-    BY[D] = BY[src & 0xFF];
+    if constexpr (BYN) BY[D] = BY[src & 0xFF];
     return;
   } else {
     BX[D] = BX[src & 0xFF] ^ mbits;
   }
+  if constexpr (!BYN) return;
   // Keep C - BX a value of its own: reassociated as (partner T - BX) + C it would put two
   // adds after the AND on the column-to-column dependency chain instead of one.
   BY[D] = C - BX[D];
@@ -208,15 +209,48 @@ __device__ __forceinline__ void column_acs(uint32_t (&M)[kDw], const uint32_t (&
 // G: wrap the metrics mod 256 after every add (two ANDs per dword).  Without it (G false)
 // the column has no AND except at KPH 0, which clears the cycle's history: see "Guard-free
 // columns" below.
+// Phases whose partner is another dword of the lane: the two dwords form butterflies with the
+// same branch-metric words (the partner's BX is BX with the markers flipped), and
+// S = T[D] + T[D'] + C serves both: T[D'] + (C - BX) = S - (T[D] + BX), so the pair needs one
+// add3 instead of two C - BX subtractions.  The 32-bit sums are the same integers as T' + BY
+// (carries between the halves cancel), so the result is bit-identical.
+template <int PH, bool G, int D>
+__device__ __forceinline__ void column_pair(uint32_t (&M)[kDw], const uint32_t (&T)[kDw], const uint32_t (&BX)[kDw],
+                                            uint32_t C) {
+  constexpr int Dp = D ^ (1 << (5 - PH - 1));
+  if constexpr (D < Dp) {
+    uint32_t S = T[D] + T[Dp] + C;
+    asm("" : "+v"(S));                                 // (else S - X folds back into T[D'] + C - BX)
+    uint32_t X = T[D] + BX[D], Xp = T[Dp] + BX[Dp];
+    uint32_t Z = S - X, Zp = S - Xp;
+    if constexpr (G) {
+      X &= 0x7FFF7FFFu;
+      Z &= 0x7FFF7FFFu;
+      Xp &= 0x7FFF7FFFu;
+      Zp &= 0x7FFF7FFFu;
+    }
+    M[D] = w32(__builtin_elementwise_min(h2(X), h2(Z)));
+    M[Dp] = w32(__builtin_elementwise_min(h2(Xp), h2(Zp)));
+  }
+}
+#ifndef ZRX_PAIR_S
+#define ZRX_PAIR_S 1
+#endif
 template <int PH, int KIND, int KPH, bool G, int... D>
 __device__ __forceinline__ void column5_(uint32_t (&M)[kDw], uint32_t P, const Consts& K, std::integer_sequence<int, D...>) {
   const uint32_t T[kDw] = {(KPH == 0 ? (M[D] & 0x7F007F00u) : M[D])...};
   constexpr uint32_t mk = 1u << KPH;
   constexpr uint32_t Kc = KIND == 0 ? 14u : 7u;        // (28 or 14) / 2: a column's complementary BM / 2
   constexpr uint32_t C = ((Kc << 8) | mk) * 0x00010001u;
+  constexpr int pb = 5 - PH;
   uint32_t BX[kDw], BY[kDw];
-  (column_bx<PH, KPH, D>(BX, BY, P, K, C), ...);
-  (column_acs<PH, G, D>(M, T, BX, BY), ...);
+  if constexpr (ZRX_PAIR_S && pb >= 1 && pb <= kDwBits) {
+    (column_bx<PH, KPH, D, false>(BX, BY, P, K, C), ...);
+    (column_pair<PH, G, D>(M, T, BX, C), ...);
+  } else {
+    (column_bx<PH, KPH, D>(BX, BY, P, K, C), ...);
+    (column_acs<PH, G, D>(M, T, BX, BY), ...);
+  }
 }
 template <int PH, int KIND, int KPH, bool G = true>
 __device__ __forceinline__ void column5(uint32_t (&M)[kDw], uint32_t P, const Consts& K) {
