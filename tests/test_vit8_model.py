@@ -26,8 +26,14 @@ def test_bx_sources_hold():
                 a, b = int(V.SEL[ph, l, d]), int(V.SEL[ph, l, src[1]])
                 if src[0] == "same":
                     assert a == b, (ph, d, l)
-                else:
+                elif src[0] == "mk":
                     assert a ^ b == ((4 ^ 12) | ((4 ^ 12) << 16)), (ph, d, l)
+                else:                                   # complement: P byte 3 - k, marker as src[2] says
+                    for h in range(2):
+                        ka, kb = (a >> (16 * h + 8)) & 3, (b >> (16 * h + 8)) & 3
+                        ma, mb = (a >> (16 * h)) & 0xFF, (b >> (16 * h)) & 0xFF
+                        assert ka == 3 - kb, (ph, d, l)
+                        assert (ma != mb) == bool(src[2]), (ph, d, l)
 
 
 @pytest.mark.parametrize("idx", range(0, 48, 3))

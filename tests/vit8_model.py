@@ -80,14 +80,21 @@ def bx_source(ph, d):
     if a_flip == 0 and b_flip == 0:
         return ("mk", 0) if m_flip else ("same", 0)
     # another dword with the same (A, B) flips, if any, lower first
-    for e in range(1, d):
+    def flips_of(e):
         fe = [(1 + ph) % 6 if e & 1 else None, (2 + ph) % 6 if e & 2 else None]
         fe = [b for b in fe if b is not None]
-        ae = sum(1 for b in fe if b in (1, 2, 4)) & 1
-        be = sum(1 for b in fe if b in (0, 1, 2)) & 1
-        me = sum(1 for b in fe if b == 5) & 1
+        return (sum(1 for b in fe if b in (1, 2, 4)) & 1, sum(1 for b in fe if b in (0, 1, 2)) & 1,
+                sum(1 for b in fe if b == 5) & 1)
+    for e in range(1, d):
+        ae, be, me = flips_of(e)
         if (ae, be) == (a_flip, b_flip):
             return ("mk", e) if me != m_flip else ("same", e)
+    # both expected bits flipped against dword e: complementary branch metrics, BX and BY swap
+    # roles (zrx_viterbi3.hpp bx_src), the markers flipped unless the marker bit flips too
+    for e in range(d):
+        ae, be, me = flips_of(e)
+        if (ae ^ a_flip, be ^ b_flip) == (1, 1):
+            return ("comp", e, me != m_flip)
     return ("perm",)
 
 
@@ -127,18 +134,26 @@ class Packet(V3.Packet):
         mk = 1 << k
         P = (V3.p_word(kind, a, b) >> 1) & 0x7F7F7F7F           # BM / 2 per byte
         BX = np.zeros((NL, ND), np.uint32)
+        BY = np.zeros((NL, ND), np.uint32)
         mbits = mk * 0x00010001
+        K = 14 if kind == V3.FULL else 7
+        C = ((K << 8) | mk) * 0x00010001
+        sub = lambda x: ((C - x.astype(np.int64)) & 0xFFFFFFFF).astype(np.uint32)
         for d in range(ND):
             src = bx_source(ph, d)
+            if src[0] == "comp":
+                fl = 0 if src[2] else mbits
+                BX[:, d], BY[:, d] = BY[:, src[1]] ^ fl, BX[:, src[1]] ^ fl
+                # (the complement identity the kernel relies on, checked on every column)
+                assert (BY[:, d] == sub(BX[:, d])).all()
+                continue
             if src[0] == "perm":
                 BX[:, d] = V3.perm(mk * 0x01010101, P, SEL[ph, :, d])
             elif src[0] == "same":
                 BX[:, d] = BX[:, src[1]]
             else:
                 BX[:, d] = BX[:, src[1]] ^ mbits
-        K = 14 if kind == V3.FULL else 7
-        C = ((K << 8) | mk) * 0x00010001
-        BY = ((C - BX.astype(np.int64)) & 0xFFFFFFFF).astype(np.uint32)
+            BY[:, d] = sub(BX[:, d])
         add = lambda x, y: ((x.astype(np.uint64) + y) & 0xFFFFFFFF).astype(np.uint32)
         wraps = lambda x: int(((x & 0x80008000) != 0).sum())
         Tp = partner(T, ph)

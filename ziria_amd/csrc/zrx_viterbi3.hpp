@@ -87,6 +87,9 @@ __host__ __device__ constexpr int partner_dpp(int pb) {
        : kLanes == 8 ? (pb == 5 ? 0x141 : pb == 4 ? 0x4E : 0xB1)
                      : (pb == 5 ? 0x128 : pb == 4 ? 0x140 : pb == 3 ? 0x4E : 0xB1);
 }
+#ifndef ZRX_BX_COMP
+#define ZRX_BX_COMP 1
+#endif
 // Branch-metric word sharing (tests/vit8_model.py bx_source): the state bits dword d's
 // position bits flip at phase ph; flipping state bit 3 changes neither expected bit, bit 5
 // only the marker, bits 1 and 2 both A and B, bit 0 B, bit 4 A (encoding.blk:92-109).
@@ -103,6 +106,9 @@ __host__ __device__ constexpr int ab_flips(uint32_t f) {
     if ((f >> i) & 1) { a ^= (i == 1 || i == 2 || i == 4); b ^= (i <= 2); }
   return 2 * a + b;
 }
+// Failing that, e | mk << 8 | 1 << 9 when dword e's states have both expected bits flipped:
+// their branch metrics are the complements, so BX and BY swap roles (BM(~A, ~B) / 2 =
+// Kc - BM(A, B) / 2, the identity BY = C - BX already rests on), the markers flipped unless mk.
 __host__ __device__ constexpr int bx_src(int ph, int d) {
   if (d == 0) return -1;
   const uint32_t f = dw_flips(ph, d);
@@ -110,6 +116,12 @@ __host__ __device__ constexpr int bx_src(int ph, int d) {
     const uint32_t fe = dw_flips(ph, e);
     if (ab_flips(f) == ab_flips(fe)) return e | (int)((((f ^ fe) >> 5) & 1u) << 8);
   }
+#if ZRX_BX_COMP
+  for (int e = 0; e < d; e++) {
+    const uint32_t fe = dw_flips(ph, e);
+    if ((ab_flips(f) ^ ab_flips(fe)) == 3) return e | (int)((((f ^ fe) >> 5) & 1u) << 8) | (1 << 9);
+  }
+#endif
   return -1;
 }
 
@@ -174,6 +186,12 @@ __device__ __forceinline__ void column_bx(uint32_t (&BX)[kDw], uint32_t (&BY)[kD
   constexpr int src = bx_src(PH, D);
   if constexpr (src < 0) {
     BX[D] = __builtin_amdgcn_perm(mk * 0x01010101u, P, K.sel[PH][D]);
+  } else if constexpr ((src >> 9) & 1) {               // complement: the roles swap
+    static_assert(BYN, "a complement source needs its BY word (pair phases compute none)");
+    constexpr uint32_t fl = ((src >> 8) & 1) ? 0u : mbits;
+    BX[D] = BY[src & 0xFF] ^ fl;
+    if constexpr (BYN) BY[D] = BX[src & 0xFF] ^ fl;
+    return;
   } else if constexpr ((src >> 8) == 0) {
     BX[D] = BX[src & 0xFF];
     if constexpr (BYN) BY[D] = BY[src & 0xFF];
