@@ -146,6 +146,12 @@ class Packet(V3.Packet):
                 BX[:, d], BY[:, d] = BY[:, src[1]] ^ fl, BX[:, src[1]] ^ fl
                 # (the complement identity the kernel relies on, checked on every column)
                 assert (BY[:, d] == sub(BX[:, d])).all()
+                if ph == 5 and not src[2]:
+                    # at the half-partner phase a word's halves hold one branch metric and the
+                    # two markers: flipping the markers swaps the halves (column_acs op_sel form)
+                    e = src[1]
+                    assert (BX[:, d] == V3.swap_halves(BY[:, e])).all()
+                    assert (BY[:, d] == V3.swap_halves(BX[:, e])).all()
                 continue
             if src[0] == "perm":
                 BX[:, d] = V3.perm(mk * 0x01010101, P, SEL[ph, :, d])

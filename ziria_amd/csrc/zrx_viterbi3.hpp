@@ -209,13 +209,23 @@ template <int PH, bool G, int D>
 __device__ __forceinline__ void column_acs(uint32_t (&M)[kDw], const uint32_t (&T)[kDw], const uint32_t (&BX)[kDw],
                                            const uint32_t (&BY)[kDw]) {
   constexpr int pb = 5 - PH;                           // partner's position bit
-  uint32_t X = T[D] + BX[D];
-  uint32_t Z;
-  if constexpr (pb == 0) {         // partner = the other half: [T.lo + BY.hi][T.hi + BY.lo] in one op
+  constexpr int src = bx_src(PH, D);
+  uint32_t X, Z;
+  if constexpr (pb == 0 && ((src >> 9) & 1) && !((src >> 8) & 1)) {
+    // partner = the other half, words the complement of dword e's: the two halves of a word
+    // then hold one branch metric and the two markers, so BX ^ markers is BX with its halves
+    // swapped, and op_sel takes e's words as they are (no v_xor)
+    constexpr int e = src & 0xFF;
+    asm("v_pk_add_u16 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0]" : "=v"(X) : "v"(T[D]), "v"(BY[e]));
+    asm("v_pk_add_u16 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,0]" : "=v"(Z) : "v"(T[D]), "v"(BX[e]));
+  } else if constexpr (pb == 0) {  // partner = the other half: [T.lo + BY.hi][T.hi + BY.lo] in one op
+    X = T[D] + BX[D];
     asm("v_pk_add_u16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(Z) : "v"(T[D]), "v"(BY[D]));
   } else if constexpr (pb <= kDwBits) {                // partner = another dword of the lane
+    X = T[D] + BX[D];
     Z = T[D ^ (1 << (pb - 1))] + BY[D];
   } else {                                             // partner lane: the DPP source of the add
+    X = T[D] + BX[D];
     Z = (uint32_t)__builtin_amdgcn_mov_dpp((int)T[D], partner_dpp(pb), 0xF, 0xF, true) + BY[D];
   }
   if constexpr (G) {                                   // the u8 wrap (bit 15 of a half)
