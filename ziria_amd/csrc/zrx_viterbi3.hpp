@@ -915,7 +915,10 @@ static __device__ __forceinline__ void ds_b8_hi(uint32_t a, uint32_t v) {
     constexpr int c = J + 1;                           // column index within the body after the step
     column5<J % 6, r, (J + 2) % 8, G>(M, P, K);
     if constexpr (CHK && (c == 6 || c == 12 || c == 18)) {   // guard-free body: some state has H <= 115
-      const uint64_t pass = __builtin_amdgcn_ballot_w64((uint16_t)M[0] < (uint16_t)0x3A00u) | dead;
+      // (one 16-bit compare into a lane mask: written as C++ it became an AND and a 32-bit compare)
+      uint64_t lt;
+      asm("v_cmp_gt_u16_e64 %0, %1, %2" : "=s"(lt) : "s"(0x3A00u), "v"(M[0]));   // (VOP3: no literal)
+      const uint64_t pass = lt | dead;
       ok = ok & rows_all_any(pass);                    // (no short-circuit: a branch would split the body)
     }
     if constexpr (c % 8 == 6 && !(DBG & 2)) {
