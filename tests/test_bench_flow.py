@@ -89,14 +89,17 @@ HARNESS = textwrap.dedent("""
     bench.txgen.make_mixed_fast = lambda n, **k: mixed(n, **{**k, "device": cpu})
     sys.argv = [os.path.abspath(__file__)] + argv
     bench.main()
-    print("LOG %s %s" % (os.environ.get("RANK", "0"), json.dumps(log)), flush=True)
+    # (each rank's log to a file of its own: ranks share the stdout pipe, and a long line of
+    # one rank can land inside another's)
+    with open(os.path.join(os.environ["ZRX_FLOW_LOGDIR"], "log_%s.json" % os.environ.get("RANK", "0")), "w") as f:
+        f.write(json.dumps(log))
 """)
 
 
 def _run(tmp_path, args):
     script = tmp_path / "bench_harness.py"
     script.write_text(f"ROOT = {ROOT!r}\n" + HARNESS)
-    env = dict(os.environ, OMP_NUM_THREADS="2")
+    env = dict(os.environ, OMP_NUM_THREADS="2", ZRX_FLOW_LOGDIR=str(tmp_path))
     env.pop("WORLD_SIZE", None)
     p = subprocess.run([sys.executable, str(script)] + args, capture_output=True, text=True, timeout=900, cwd=ROOT,
                        env=env)
@@ -104,10 +107,8 @@ def _run(tmp_path, args):
     lines = p.stdout.splitlines()
     line = json.loads(next(x for x in lines if x.startswith("{")))
     logs = {}
-    for x in lines:
-        if x.startswith("LOG "):
-            rank, js = x[4:].split(" ", 1)
-            logs[int(rank)] = json.loads(js)
+    for f in tmp_path.glob("log_*.json"):
+        logs[int(f.stem[4:])] = json.loads(f.read_text())
     return line, logs
 
 
