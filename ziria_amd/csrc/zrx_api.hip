@@ -366,7 +366,7 @@ static void launch_viterbi(zrx_ctx* c, const uint8_t* soft, const int64_t* soft_
 #ifdef ZRX_EXPERIMENTS
   switch (c->v3dbg) {   // timing experiments (ZRX_V3DBG); 0 is the product kernel
 #define ZRX_V3(D) case D: k_viterbi3<D><<<g, b, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits, rows, nrows, nullptr, c->dumps); return;
-    ZRX_V3(1) ZRX_V3(2) ZRX_V3(4) ZRX_V3(8) ZRX_V3(16) ZRX_V3(64) ZRX_V3(1024) ZRX_V3(1032)
+    ZRX_V3(1) ZRX_V3(2) ZRX_V3(4) ZRX_V3(8) ZRX_V3(16) ZRX_V3(64) ZRX_V3(1024) ZRX_V3(1032) ZRX_V3(2048)
 #undef ZRX_V3
     default: break;
   }

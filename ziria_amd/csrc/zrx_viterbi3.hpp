@@ -631,8 +631,13 @@ struct Walk {
   uint32_t ix, b, acc, voff;      // per lane: ring index (row offset included), pending byte, dword, store offset
   uint64_t ob;                    // wave-uniform: output base the store offsets are relative to
 };
+// (The base is re-read as wave-uniform here: built from the struct field as it is, the
+// descriptor was not provably uniform across the body's control flow, and every store became
+// a waterfall loop of readfirstlanes, 64-bit compares and exec updates.)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t walk_rsrc(const Walk& W) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)W.ob, (short)0, 0x7FFFFFFF, 0x00020000);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)W.ob);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(W.ob >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, 0x7FFFFFFF, 0x00020000);
 }
 // The setup runs in a branch whose join the divergence analysis cannot prove uniform; the
 // scalar fields are uniform by construction, so they are re-read as such.
@@ -644,14 +649,18 @@ __device__ __forceinline__ void walk_uniform(Walk& W) {
 }
 
 // One walk step t (compile-time when called from the body columns).
-template <class I>
+template <bool FAKE = false, class I>
 __device__ __forceinline__ void walk_stepk(Walk& W, I t, uint32_t nl, const uint8_t* ring0, uint32_t rb) {
   constexpr uint32_t span = (uint32_t)kRing * kSlotBytes;
   const uint32_t b = W.b;
   W.acc = (W.acc << 8) | b;                            // lookahead bytes leave before the first store
   W.ix = (b & 63u) | rb;
   W.A = W.A == 0u ? span - (uint32_t)kSlotBytes : W.A - (uint32_t)kSlotBytes;
-  if (t + 1 < nl + 32u) W.b = ring0[W.A + W.ix];
+  if constexpr (FAKE) {                                // (timing experiment: no LDS read on the chain)
+    if (t + 1 < nl + 32u) W.b = (W.ix * 5u + W.A) & 0xFFu;
+  } else {
+    if (t + 1 < nl + 32u) W.b = ring0[W.A + W.ix];
+  }
   if (t >= nl && ((t - nl) & 3u) == 3u)                // output bytes 31-o .. 34-o, o = t - nl
     __builtin_amdgcn_raw_buffer_store_b32(W.acc, walk_rsrc(W), (int)(W.voff + 31u - (t - nl)), 0, 0);
 }
@@ -851,11 +860,12 @@ struct Packet {
   // columns 0..11, step J + 12 after, NL + 32 steps in all.
   template <int J, int NL>
   __device__ __forceinline__ void walk_col() {
+    constexpr bool fake = (DBG & 2048) != 0;
     if constexpr (J < 12) {
-      walk_stepk(*W, (uint32_t)(2 * J), (uint32_t)NL, ring0, rib * 64u);
-      walk_stepk(*W, (uint32_t)(2 * J + 1), (uint32_t)NL, ring0, rib * 64u);
+      walk_stepk<fake>(*W, (uint32_t)(2 * J), (uint32_t)NL, ring0, rib * 64u);
+      walk_stepk<fake>(*W, (uint32_t)(2 * J + 1), (uint32_t)NL, ring0, rib * 64u);
     } else if constexpr (J + 12 < NL + 32) {
-      walk_stepk(*W, (uint32_t)(J + 12), (uint32_t)NL, ring0, rib * 64u);
+      walk_stepk<fake>(*W, (uint32_t)(J + 12), (uint32_t)NL, ring0, rib * 64u);
     }
   }
   // The half-1 snapshot bytes go out by asm without a memory clobber (one clobber per store
@@ -1452,6 +1462,9 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
         const bool mixed = rows != nullptr && uni == 0u;
         const bool lrpt = !FIX && (v3::kPrioMode == 2 || (v3::kPrioMode == 3 && mixed));
         const bool younger = !FIX && (v3::kPrioMode == 1 || (v3::kPrioMode == 3 && !mixed)) && ((blockIdx.x / ncu) & 1u) != 0u;
+#if defined(ZRX_STAGGER) && ZRX_STAGGER > 0
+        if (younger) __builtin_amdgcn_s_sleep(ZRX_STAGGER);   // (experiment: offset the SIMD's two waves)
+#endif
         v3::Row Rr;
         Rr.ob = xfix ? xw - v3::seg_cmp(xw) : xk ? xw : 0u;
         Rr.end = x.E - x.S; Rr.cols = colsS;
