@@ -684,18 +684,23 @@ __device__ __forceinline__ void traceback(bool due, const uint32_t (&M)[kDw], ui
                                           uint8_t* __restrict__ out, uint32_t ooff, uint32_t& nbytes,
                                           Walk* W = nullptr, uint32_t tr0 = 0) {
   const uint32_t ph = T % 6u;
+  // H in bits 14..8 (halved), the marker of column T at bit (T+1)%8; the n = (T-6)%8 newest
+  // decisions in bits n-1..0
+  const uint32_t n = (T - 6u) & 7u, ms = (T + 1u) & 7u;
+  // the state of half q: pos_of(l, q >> 1, q & 1) = pos_of(l, 0, 0) ^ q, and rotl6 is linear
+  // over XOR, so st(q) = rotl6(pos_of(l, 0, 0), ph) ^ rotl6(q, ph)
+  const uint32_t st0 = rotl6(pos_of(l, 0, 0), ph);
+  const uint32_t r0 = rotl6(1u, ph), r1 = rotl6(2u, ph), r2 = rotl6(4u, ph);
   uint32_t best = 0xFFFFFFFFu;
 #pragma unroll
   for (int q = 0; q < 2 * kDw; q++) {
     const uint32_t half = M[q >> 1] >> (16 * (q & 1)) & 0xFFFFu;
-    const uint32_t st = rotl6(pos_of(l, q >> 1, q & 1), ph);
-    // H in bits 14..8 (halved), the marker of column T at bit (T+1)%8; the n = (T-6)%8 newest
-    // decisions in bits n-1..0
-    const uint32_t n = (T - 6u) & 7u;
-    const uint32_t m = ((half >> 7) & 0xFEu) | ((half >> ((T + 1u) & 7u)) & 1u);
+    const uint32_t st = st0 ^ ((q & 1) ? r0 : 0u) ^ ((q & 2) ? r1 : 0u) ^ ((q & 4) ? r2 : 0u);
     const uint32_t pad = ((half & ((1u << n) - 1u)) << (8u - n)) & 0xFFu;   // as the shifted pad: newest at bit 7
-    const uint32_t ukey = (((m << 8) | (st << 2)) & 0xFFFFu) ^ 0x8000u;   // signed int16 order
-    best = min(best, (ukey << 16) | pad);
+    // the key (m << 8 | 4 st) in signed int16 order, m = H | marker, above the pad:
+    // [H bits 7..1 ^ sign][marker][st][0 0][pad]
+    const uint32_t key = (((half & 0x7F00u) << 17) | (((half >> ms) & 1u) << 24) | (st << 18) | pad) ^ 0x80000000u;
+    best = min(best, key);
   }
   best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0xB1, 0xF, 0xF, false));
   best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x4E, 0xF, 0xF, false));
