@@ -1264,12 +1264,15 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
     }
     if constexpr ((DBG & 1) != 0) R.ppend = R.fpend = false;
     next_body();
-    // A deferred traceback walk runs in the next body's columns (checked: rare).
+    // A deferred traceback walk runs in the next body's columns.
     if (W.we && __builtin_amdgcn_ballot_w64(R.live) != 0) {
       uint32_t Pw[kPw];
       publish();
       pwords(Pw, base);
       pk.ring = ring_block + slot * kSlotBytes;
+      // No event due in this body (the usual case: a wave's windows end together, one body
+      // before): the walk rides an unchecked body, and only the metrics need a copy.
+      const bool quiet = s_next > tr0 + 24 && s_next != kNever;
       if constexpr (CR == 2 && kNoGuard) {
         // speculative: on a failed check the body is redone without the walk, whose reads all
         // came before this body's snapshot stores and from verified bodies' slots (Walk), so
@@ -1277,20 +1280,34 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
         uint32_t M0[kDw];
 #pragma unroll
         for (int d = 0; d < kDw; d++) M0[d] = M[d];
-        const Row R0 = R;
-        const RowX x0 = rowx[rib];
-        const uint32_t s0 = s_next;
-        const uint64_t dead = __builtin_amdgcn_ballot_w64(!R.live);
-        const bool ok = W.we == 3 ? pk.template body<true, 3, false, true>(M, Pw, tr0, s_next, cols24, dead)
-                                  : pk.template body<true, 2, false, true>(M, Pw, tr0, s_next, cols24, dead);
-        if (!ok) {
+        if (quiet) {
+          const uint64_t dead = __builtin_amdgcn_ballot_w64(!R.live);
+          const bool ok = W.we == 3 ? pk.template body<false, 3, false, true>(M, Pw, tr0, s_next, cols24, dead)
+                                    : pk.template body<false, 2, false, true>(M, Pw, tr0, s_next, cols24, dead);
+          if (!ok) {
 #pragma unroll
-          for (int d = 0; d < kDw; d++) M[d] = M0[d];
-          R = R0;
-          rowx[rib] = x0;
-          s_next = s0;
-          pk.template body<true, 0, true, false>(M, Pw, tr0, s_next, cols24);
+            for (int d = 0; d < kDw; d++) M[d] = M0[d];
+            pk.template body<false, 0, true, false>(M, Pw, tr0, s_next, cols24);
+          }
+        } else {
+          const Row R0 = R;
+          const RowX x0 = rowx[rib];
+          const uint32_t s0 = s_next;
+          const uint64_t dead = __builtin_amdgcn_ballot_w64(!R.live);
+          const bool ok = W.we == 3 ? pk.template body<true, 3, false, true>(M, Pw, tr0, s_next, cols24, dead)
+                                    : pk.template body<true, 2, false, true>(M, Pw, tr0, s_next, cols24, dead);
+          if (!ok) {
+#pragma unroll
+            for (int d = 0; d < kDw; d++) M[d] = M0[d];
+            R = R0;
+            rowx[rib] = x0;
+            s_next = s0;
+            pk.template body<true, 0, true, false>(M, Pw, tr0, s_next, cols24);
+          }
         }
+      } else if (quiet) {
+        if (W.we == 3) pk.template body<false, 3, kG, false>(M, Pw, tr0, s_next, cols24);
+        else pk.template body<false, 2, kG, false>(M, Pw, tr0, s_next, cols24);
       } else {
         if (W.we == 3) pk.template body<true, 3, kG, false>(M, Pw, tr0, s_next, cols24);
         else pk.template body<true, 2, kG, false>(M, Pw, tr0, s_next, cols24);
