@@ -57,6 +57,7 @@ constexpr int kWavesPerSimd = kLanes == 4 ? 1 : kLanes == 8 ? 2 : 4;   // LDS ri
 constexpr uint32_t kNever = 0x7FFFFFFFu;
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u16x2 h2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
 __device__ __forceinline__ uint32_t w32(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
 
@@ -689,27 +690,71 @@ __device__ __forceinline__ void traceback(bool due, const uint32_t (&M)[kDw], ui
   const uint32_t n = (T - 6u) & 7u, ms = (T + 1u) & 7u;
   // the state of half q: pos_of(l, q >> 1, q & 1) = pos_of(l, 0, 0) ^ q, and rotl6 is linear
   // over XOR, so st(q) = rotl6(pos_of(l, 0, 0), ph) ^ rotl6(q, ph)
-  const uint32_t st0 = rotl6(pos_of(l, 0, 0), ph);
-  const uint32_t r0 = rotl6(1u, ph), r1 = rotl6(2u, ph), r2 = rotl6(4u, ph);
-  uint32_t best = 0xFFFFFFFFu;
+  // rotl6(x, ph) = bits 6 - ph .. 11 - ph of (x x) = 65 x: one shift of the doubled label
+  const uint32_t o = 6u - ph;
+  const uint32_t st0 = ((pos_of(l, 0, 0) * 65u) >> o) & 63u;
+  const uint32_t r0 = (65u >> o) & 63u, r1 = (130u >> o) & 63u, r2 = (260u >> o) & 63u;
+  uint32_t s0, pad;
+  bool walker;
+  uint64_t wm;
+  if constexpr (kDw == 4) {
+    // 16-bit keys, both halves of a dword at once: [H bits 7..1][marker][st][0 0], in signed
+    // int16 order (the 32-bit key below without its pad byte; st is unique in the row, so
+    // the pad never decides).  The winner's pad is then read from the lane that holds it.
+    const uint32_t sh = 8u - ms;                       // marker bit ms -> bit 8 of each half
+    const uint32_t c0 = (st0 << 2) | ((st0 ^ r0) << 18);   // st of halves (2d, 2d + 1), at bits 2, 18
+    const uint32_t rr1 = r1 * 0x40004u, rr2 = r2 * 0x40004u;
+    const uint32_t stc[4] = {c0, c0 ^ rr1, c0 ^ rr2, c0 ^ rr1 ^ rr2};
+    i16x2 acc;
 #pragma unroll
-  for (int q = 0; q < 2 * kDw; q++) {
-    const uint32_t half = M[q >> 1] >> (16 * (q & 1)) & 0xFFFFu;
-    const uint32_t st = st0 ^ ((q & 1) ? r0 : 0u) ^ ((q & 2) ? r1 : 0u) ^ ((q & 4) ? r2 : 0u);
-    const uint32_t pad = ((half & ((1u << n) - 1u)) << (8u - n)) & 0xFFu;   // as the shifted pad: newest at bit 7
-    // the key (m << 8 | 4 st) in signed int16 order, m = H | marker, above the pad:
-    // [H bits 7..1 ^ sign][marker][st][0 0][pad]
-    const uint32_t key = (((half & 0x7F00u) << 17) | (((half >> ms) & 1u) << 24) | (st << 18) | pad) ^ 0x80000000u;
-    best = min(best, key);
+    for (int d = 0; d < 4; d++) {
+      const uint32_t y = ((M[d] << sh) & 0x01000100u) | stc[d];
+      const i16x2 k = __builtin_bit_cast(i16x2, ((M[d] << 1) & 0xFE00FE00u) | y);
+      acc = d == 0 ? k : __builtin_elementwise_min(acc, k);
+    }
+    int32_t kb = min((int32_t)acc.x, (int32_t)acc.y);
+    kb = min(kb, __builtin_amdgcn_update_dpp(0, kb, 0xB1, 0xF, 0xF, false));
+    kb = min(kb, __builtin_amdgcn_update_dpp(0, kb, 0x4E, 0xF, 0xF, false));
+    kb = min(kb, __builtin_amdgcn_update_dpp(0, kb, 0x141, 0xF, 0xF, false));
+    walker = due && l == 0 && cnt != 0;
+    wm = __builtin_amdgcn_ballot_w64(walker);
+    if (wm == 0) return;
+    s0 = ((uint32_t)kb >> 2) & 63u;
+    // the winner's half q in its lane: q = rotr6(s0 ^ st0, ph) < 8 (position bits 0..2);
+    // the row's 8 pad bytes in byte order q, one v_perm picks it, the other lanes give 0
+    const uint32_t x = (s0 ^ st0) * 65u;               // (x x): rotr6 is one bit-field extract
+    const uint32_t q = (x >> ph) & 63u;
+    const uint32_t pk0 = __builtin_amdgcn_perm(M[1], M[0], 0x06040200u);
+    const uint32_t pk1 = __builtin_amdgcn_perm(M[3], M[2], 0x06040200u);
+    const uint32_t in_lane = (uint32_t)((int32_t)(q - 8u) >> 31);
+    uint32_t pb = __builtin_amdgcn_perm(pk1, pk0, q) & in_lane & 0xFFu;
+    pb |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pb, 0xB1, 0xF, 0xF, false);
+    pb |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pb, 0x4E, 0xF, 0xF, false);
+    pb |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pb, 0x141, 0xF, 0xF, false);
+    pad = (pb << (8u - n)) & 0xFFu;                    // as the shifted pad: newest at bit 7
+  } else {
+    uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+    for (int q = 0; q < 2 * kDw; q++) {
+      const uint32_t half = M[q >> 1] >> (16 * (q & 1)) & 0xFFFFu;
+      const uint32_t st = st0 ^ ((q & 1) ? r0 : 0u) ^ ((q & 2) ? r1 : 0u) ^ ((q & 4) ? r2 : 0u) ^
+                          ((q & 8) ? (520u >> o) & 63u : 0u);
+      const uint32_t pd = ((half & ((1u << n) - 1u)) << (8u - n)) & 0xFFu;   // as the shifted pad: newest at bit 7
+      // the key (m << 8 | 4 st) in signed int16 order, m = H | marker, above the pad:
+      // [H bits 7..1 ^ sign][marker][st][0 0][pad]
+      const uint32_t key = (((half & 0x7F00u) << 17) | (((half >> ms) & 1u) << 24) | (st << 18) | pd) ^ 0x80000000u;
+      best = min(best, key);
+    }
+    best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0xB1, 0xF, 0xF, false));
+    best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x4E, 0xF, 0xF, false));
+    if constexpr (kLanes >= 8) best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x141, 0xF, 0xF, false));
+    if constexpr (kLanes == 16) best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x140, 0xF, 0xF, false));
+    walker = due && l == 0 && cnt != 0;
+    wm = __builtin_amdgcn_ballot_w64(walker);
+    if (wm == 0) return;
+    s0 = (best >> 18) & 63u;
+    pad = best & 0xFFu;
   }
-  best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0xB1, 0xF, 0xF, false));
-  best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x4E, 0xF, 0xF, false));
-  if constexpr (kLanes >= 8) best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x141, 0xF, 0xF, false));
-  if constexpr (kLanes == 16) best = min(best, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)best, 0x140, 0xF, 0xF, false));
-  const bool walker = due && l == 0 && cnt != 0;
-  const uint64_t wm = __builtin_amdgcn_ballot_w64(walker);
-  if (wm == 0) return;
-  const uint32_t s0 = (best >> 18) & 63u, pad = best & 0xFFu;
   // bit i of Z = decision of column T + 6 - i along the best path (state bits, then the pad)
   const uint32_t Z = s0 | ((__builtin_bitreverse32(pad) >> 24) << 6);
   const uint32_t C0 = T - ((T - 6u) & 7u);             // newest snapshot column <= T
