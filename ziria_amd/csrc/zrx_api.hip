@@ -424,9 +424,9 @@ int zrx_create(zrx_ctx** out, int device, void* stream) {
   // k_data_fft loops its waves over the batch: launch exactly the blocks that are resident at
   // once (occupancy from its VGPRs and LDS), so no second round of blocks runs alone at the end
   int occ = 0;
-  ZRX_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_data_fft<false>, 256, 0));
+  ZRX_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_data_fft<false>, kDfThreads, 0));
   c->df_blocks = std::max(1, occ) * c->ncu;
-  ZRX_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_data_fft<true>, 256, 0));
+  ZRX_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_data_fft<true>, kDfThreads, 0));
   c->df_blocks_eq = std::max(1, occ) * c->ncu;
 #ifdef ZRX_EXPERIMENTS
   if (const char* v = std::getenv("ZRX_V3DBG")) c->v3dbg = std::atoi(v);
@@ -730,17 +730,17 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
                                 split ? 1 : 0, ordered ? c->mixed_hint_dev : nullptr);
   if (ev) ZRX_CHECK(hipEventRecord(ev[2], h));
   // k_data_fft: waves over the batch's data symbols, at most npkts x (max_nsym - 1) of them
-  const int fft_blocks = (int)std::min<int64_t>(((int64_t)npkts * (max_nsym - 1) + 255) / 256,
+  const int fft_blocks = (int)std::min<int64_t>(((int64_t)npkts * (max_nsym - 1) + kDfThreads - 1) / kDfThreads,
                                                 (int64_t)(chan ? c->df_blocks_eq : c->df_blocks));
   zrx_ctx* const peer = c->peer;
   // (a never-recorded peer event is complete: the first batch waits for nothing)
   if (peer && (c->link_mode & 2)) ZRX_CHECK(hipStreamWaitEvent(h, peer->ev_vit_done, 0));
   if (fft_blocks > 0) {
     if (chan)
-      k_data_fft<true><<<fft_blocks, 256, 0, h>>>((const uint4*)d_sym, d_sym_off, c->vparams, npkts, (uint4*)c->soft,
+      k_data_fft<true><<<fft_blocks, kDfThreads, 0, h>>>((const uint4*)d_sym, d_sym_off, c->vparams, npkts, (uint4*)c->soft,
                                                    c->soft_off, c->dsym, c->wave_p0, chan, T);
     else
-      k_data_fft<false><<<fft_blocks, 256, 0, h>>>((const uint4*)d_sym, d_sym_off, c->vparams, npkts, (uint4*)c->soft,
+      k_data_fft<false><<<fft_blocks, kDfThreads, 0, h>>>((const uint4*)d_sym, d_sym_off, c->vparams, npkts, (uint4*)c->soft,
                                                     c->soft_off, c->dsym, c->wave_p0, chan, T);
   }
   if (ev) ZRX_CHECK(hipEventRecord(ev[3], h));

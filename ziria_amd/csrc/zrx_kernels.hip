@@ -593,10 +593,22 @@ __global__ __launch_bounds__(1024) void k_pkt_rows(const int32_t* __restrict__ v
 // on another: LDS is in order within a wave, so there are no barriers.  (Tried and dropped,
 // symbol loads by LDS-DMA, with and without a one-iteration prefetch; soft rows
 // stored by each lane.)
-constexpr int kDfWaves = 4;           // waves per block
-constexpr int kDfRow = 19;            // output staging row stride, 16-B units (a soft row is <= 18)
+#ifndef ZRX_DF_WAVES
+#define ZRX_DF_WAVES 4
+#endif
+#ifndef ZRX_DF_ROW
+#define ZRX_DF_ROW 19
+#endif
+#ifndef ZRX_DF_LUTC
+#define ZRX_DF_LUTC 4
+#endif
+constexpr int kDfWaves = ZRX_DF_WAVES;    // waves per block
+constexpr int kDfThreads = 64 * kDfWaves;
+constexpr int kDfRow = ZRX_DF_ROW;        // output staging row stride, 16-B units (a soft row is <= 18)
 constexpr int kDfUnits = 64 * kDfRow;
-constexpr int kDfLutCopies = 4;       // demap LUT copies (lane & 3): fewer LDS bank conflicts
+constexpr int kDfLutCopies = ZRX_DF_LUTC; // demap LUT copies (lane & (copies - 1)): fewer LDS bank conflicts
+static_assert(kDfRow >= 18 && (kDfLutCopies == 1 || kDfLutCopies == 2 || kDfLutCopies == 4) && 256 % kDfThreads == 0,
+              "data FFT LDS layout");
 
 __device__ __forceinline__ int soft_units_of(int mod) { return mod == 0 ? 3 : mod == 1 ? 6 : mod == 2 ? 12 : 18; }
 
@@ -659,19 +671,22 @@ __device__ __forceinline__ DfSym df_finish(const DfNext& n) {
 // over many waves and consecutive lanes write consecutive soft rows.  Waves loop over w with
 // the grid's stride (the host sizes the grid from the call's max_nsym, an upper bound).
 template <bool EQ>
-__global__ __launch_bounds__(256) void k_data_fft(const uint4* __restrict__ sym, const int64_t* __restrict__ sym_off,
+__global__ __launch_bounds__(kDfThreads) void k_data_fft(const uint4* __restrict__ sym, const int64_t* __restrict__ sym_off,
                                                   const int32_t* __restrict__ vparams, int npkts,
                                                   uint4* __restrict__ soft, const int64_t* __restrict__ soft_off,
                                                   const int32_t* __restrict__ dsym, const int32_t* __restrict__ wave_p0,
                                                   const uint32_t* __restrict__ chan, EqTabs T) {
   __shared__ uint4 stage_all[kDfWaves][kDfUnits];
-  __shared__ uint4 lut_all4[256];                     // kDfLutCopies (4) copies of entry i at 4i ..
-  static_assert(kDfLutCopies == 4, "one uint4 per LUT entry");
+  __shared__ __attribute__((aligned(16))) uint32_t lut_all[256 * kDfLutCopies];   // copies of entry i at i * copies ..
   {
-    const uint32_t v = kDemapLut[threadIdx.x];         // (256 threads: one entry each, one latency)
-    lut_all4[threadIdx.x] = make_uint4(v, v, v, v);
+    uint32_t v[256 / kDfThreads];                      // (every load in flight, then the stores)
+#pragma unroll
+    for (int j = 0; j < 256 / kDfThreads; j++) v[j] = kDemapLut[threadIdx.x + j * kDfThreads];
+#pragma unroll
+    for (int j = 0; j < 256 / kDfThreads; j++)
+#pragma unroll
+      for (int c = 0; c < kDfLutCopies; c++) lut_all[(threadIdx.x + j * kDfThreads) * kDfLutCopies + c] = v[j];
   }
-  const uint32_t* lut_all = (const uint32_t*)lut_all4;
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
