@@ -185,13 +185,14 @@ __device__ __forceinline__ void column_bx(uint32_t (&BX)[kDw], uint32_t (&BY)[kD
   constexpr uint32_t mk = 1u << KPH;
   constexpr uint32_t mbits = mk * 0x00010001u;
   constexpr int src = bx_src(PH, D);
-  if constexpr (src < 0) {
+  // (a complement source needs its BY word, which pair phases do not compute: own v_perm then;
+  // it happens only with 4-lane rows, whose pair phases have three dword bits)
+  if constexpr (src < 0 || (((src >> 9) & 1) && !BYN)) {
     BX[D] = __builtin_amdgcn_perm(mk * 0x01010101u, P, K.sel[PH][D]);
   } else if constexpr ((src >> 9) & 1) {               // complement: the roles swap
-    static_assert(BYN, "a complement source needs its BY word (pair phases compute none)");
     constexpr uint32_t fl = ((src >> 8) & 1) ? 0u : mbits;
     BX[D] = BY[src & 0xFF] ^ fl;
-    if constexpr (BYN) BY[D] = BX[src & 0xFF] ^ fl;
+    BY[D] = BX[src & 0xFF] ^ fl;
     return;
   } else if constexpr ((src >> 8) == 0) {
     BX[D] = BX[src & 0xFF];
