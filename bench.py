@@ -91,6 +91,9 @@ def main():
                     help="TX chain (transmitter() at 40 MHz, SURVEY §8f row 4) on config-3 packets")
     ap.add_argument("--eq", action="store_true",
                     help="config 3 through a channel, with ChannelEqualization + PilotTrack (SURVEY §8f row 1)")
+    ap.add_argument("--no-sub", action="store_true",
+                    help="skip the secondary workloads (configs 2 and 5, the 2048/4096-packet shards) the default "
+                         "one-GPU line carries as sub_results")
     ap.add_argument("--e2e", action="store_true",
                     help="config 3 end to end from host memory through __ext_wifi_rx_batch (SURVEY §8d: kernel-only "
                          "vs end-to-end incl. H2D from pinned memory)")
@@ -138,6 +141,11 @@ def main():
     cpu = None                                         # (the CPU baseline: rank 0 of an N = 1 run only)
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(head["batch0"], args.cpu_seconds, head["batch0"].get("chan"))
+    ranks = rank_devices(dev, head["rank_elapsed_s"], local)
+    subs = None
+    if world == 1 and not args.no_sub and not args.eq and not args.total and not args.share_gpu:
+        head.pop("batch0", None)
+        subs = sub_results(args, dev)
 
     if rank == 0:
         line = {
@@ -164,8 +172,13 @@ def main():
             "roofline": head["roofline"],
             "roofline_fft": head["roofline_fft"],
             "gather_ms": head["gather_ms"],
+            "step_stats": head["step_stats"],
+            "step_stats_one_engine": head["step_stats_one_engine"],
+            "devices": ranks,
             "cpu_baseline": cpu,
         }
+        if subs is not None:
+            line["sub_results"] = subs
         if world > 1:
             line["ranks"] = world
             line["cpu_baseline_note"] = "timed at N = 1 only: see the one-GPU line"
@@ -174,7 +187,7 @@ def main():
                                        "copies); the ranks contend for one GPU, so this is no scaling point")
         if strong is not None:
             line["strong"] = {k: strong[k] for k in ("value", "ms_per_step", "value_one_engine", "bit_exact_check",
-                                                     "gather_ms")}
+                                                     "gather_ms", "step_stats", "rank_elapsed_s")}
             line["strong"].update(scaling="strong", config=strong["config"],
                                   what="config 4 as SURVEY §8(d) defines it: config 3's 16384 packets split over "
                                        f"the {world} ranks, timed in the same run after the weak-scaling headline")
@@ -228,9 +241,15 @@ def rx_run(args, total, world, rank, local, dev):
         with torch.cuda.stream(streams[j]):
             engs[j].rx(x["sym"], x["sym_off"], x["nsym"], state["S"], state["outs"][j][0], state["outs"][j][1],
                        chan=x.get("chan"))
+        state["last_stream"] = streams[j]
 
     def step(sh, k):
         run_on(k % len(engs), k % nb)
+
+    clock = StepClock(args.steps)
+
+    def on_step(i):
+        clock.mark(i, None if i < 0 else state["last_stream"])
 
     # stage times: a separate instrumented pass of engine 0 alone over the rotating batches,
     # after the warmup and before the timed steps (the pipelined steps overlap, so their
@@ -267,7 +286,8 @@ def rx_run(args, total, world, rank, local, dev):
     res = node.run_sharded(total, make_shard, step, outputs,
                            lambda lo, hi, bi: txgen.payloads_range(lo, hi, args.payload, seed=0x5EED + bi),
                            args.steps, args.warmup, args.payload, device=dev, crc_ok_only=args.eq,
-                           on_timed=instrumented, nbatches=nb)
+                           on_timed=instrumented, nbatches=nb, on_step=on_step)
+    step_stats = clock.stats()
     stage = state["stage"]
     n, S = res["hi"] - res["lo"], state["S"]
     for e in engs:                                         # the Viterbi plans dropped no rows (ZRX_EPLAN)
@@ -280,12 +300,16 @@ def rx_run(args, total, world, rank, local, dev):
         run_on(0, k % nb)
     torch.cuda.synchronize(dev)
     node.barrier(dev)
+    clock1 = StepClock(args.steps)
     t0 = time.perf_counter()
+    clock1.mark(-1)
     for k in range(args.steps):
         run_on(0, k % nb)
+        clock1.mark(k, streams[0])
     torch.cuda.synchronize(dev)
     node.barrier(dev)
     single = node.max_over_ranks(time.perf_counter() - t0, device=dev)
+    step_stats_one = clock1.stats()
 
     decoded_bits = n * (args.payload + 4 + 2) * 8          # Viterbi output bits per launch (this rank)
     vit_ms = stage["data_viterbi"]
@@ -324,6 +348,9 @@ def rx_run(args, total, world, rank, local, dev):
                          "traffic": None if args.eq else traffic_for("k_data_fft", n),
                          "units": f"544 B per data symbol x {n * nsym_data} symbols/launch"},
         "gather_ms": round(res["gather_s"] * 1e3, 3),
+        "step_stats": step_stats,
+        "step_stats_one_engine": step_stats_one,
+        "rank_elapsed_s": [round(x, 6) for x in res["rank_elapsed"]],
     }
     if rank == 0:
         out["bit_exact_check"] = {"crc_pass": res["ok"], "packets": res["packets"],
@@ -334,6 +361,43 @@ def rx_run(args, total, world, rank, local, dev):
                                                 "transmitted payload"}
     for e in engs:
         e.close()
+    return out
+
+
+def rank_devices(dev, rank_elapsed, local):
+    """Per rank: its device index and PCI address (all-gathered, so a multi-GPU record shows
+    that the ranks ran on distinct GPUs) and its own elapsed time over the timed region."""
+    p = torch.cuda.get_device_properties(dev)
+    mine = [float(local), float(p.pci_domain_id), float(p.pci_bus_id), float(p.pci_device_id)]
+    allr = node.all_gather_floats(mine, device=dev)
+    return [{"rank": r, "device": int(v[0]), "pci": "%04x:%02x:%02x.0" % (int(v[1]), int(v[2]), int(v[3])),
+             "name": p.name if r == 0 else None, "elapsed_s": rank_elapsed[r] if r < len(rank_elapsed) else None}
+            for r, v in enumerate(allr)]
+
+
+def sub_results(args, dev):
+    """The secondary workloads on the same GPU, each with its own timing and bit-exact check,
+    for the driver's one-GPU line: BASELINE config 2 (batched Viterbi alone), config 5 (mixed
+    MCS), and config 4's shard sizes at 4 and 8 GPUs (2048 / 4096 packets of config 3 on one
+    GPU).  The same --steps / --warmup; no CPU baselines (the headline carries its own)."""
+    out = {}
+    a = argparse.Namespace(**vars(args))
+    t0 = time.perf_counter()
+    keep = ("value", "unit", "ms_per_step", "value_one_engine", "bit_exact_check", "stage_ms", "step_stats",
+            "pipeline", "config")
+    r = bench_viterbi_only(a, emit=False, cpu=False)
+    out["config2"] = {k: r[k] for k in keep if k in r}
+    r = bench_mixed(a, emit=False, cpu=False)
+    out["config5"] = {k: r[k] for k in keep if k in r}
+    for g in (8, 4):                                    # (2048 / 4096 packets at config 3's 16384)
+        n = max(1, args.npkts // g)
+        r = rx_run(a, n, 1, 0, dev.index or 0, dev)
+        r.pop("batch0", None)
+        out[f"shard_{n}"] = dict({k: r[k] for k in keep if k in r}, unit="Mbit/s",
+                                 step_stats_one_engine=r["step_stats_one_engine"],
+                                 what=f"config 4's per-GPU shard at {g} GPUs: {n} config-3 packets")
+        torch.cuda.empty_cache()
+    out["wall_s"] = round(time.perf_counter() - t0, 1)
     return out
 
 
@@ -357,18 +421,56 @@ def spawn_ranks(n):
     sys.exit(rc)
 
 
-def _timed(step, steps, warmup):
+class StepClock:
+    """Per-step times inside a timed region, so that a stall shows on the line that had it: a
+    HIP event recorded after every step on the stream that ran it (events created before the
+    region) and the host clock at the same points.  gpu_step_ms are the gaps between
+    consecutive step completions on the GPU; host_issue_ms the host time spent issuing each
+    step (a host that issues slower than the GPU decodes starves the GPU)."""
+
+    def __init__(self, steps):
+        self.ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+        for e in self.ev:                                # (the HIP events exist before the region)
+            e.record()
+        torch.cuda.synchronize()
+        self.host = [0.0] * (steps + 1)
+
+    def mark(self, i, stream=None):
+        """i = -1 at the start of the region, else after timed step i (on its stream)."""
+        self.ev[i + 1].record(stream if stream is not None else torch.cuda.current_stream())
+        self.host[i + 1] = time.perf_counter()
+
+    def stats(self):
+        torch.cuda.synchronize()
+        done = sorted(self.ev[0].elapsed_time(e) for e in self.ev[1:])
+        g = np.diff([0.0] + done)
+        h = np.diff(self.host) * 1e3
+        q = lambda a, f: round(float(f(a)), 4) if len(a) else None
+        return {"gpu_step_ms": {"min": q(g, np.min), "median": q(g, np.median), "max": q(g, np.max),
+                                "mean": q(g, np.mean)},
+                "host_issue_ms": {"median": q(h, np.median), "max": q(h, np.max)},
+                "slowest_step": int(np.argmax(g)) if len(g) else None,
+                "how": "HIP event after each timed step on its stream; gaps between consecutive completions"}
+
+
+def _timed(step, steps, warmup, clock=None):
+    """warmup untimed steps, then `steps` timed ones; step() returns the stream it launched on
+    (or None), which the clock records on."""
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
+    if clock:
+        clock.mark(-1)
+    for i in range(steps):
+        st = step()
+        if clock:
+            clock.mark(i, st)
     torch.cuda.synchronize()
     return time.perf_counter() - t0
 
 
-def bench_viterbi_only(args):
+def bench_viterbi_only(args, emit=True, cpu=True):
     """BASELINE config 2: 4096 frames of 1500 bytes, rate 1/2, soft = 7*bit + U[-2,2] clipped
     to [0,7], 24048 soft values per frame (48-value groups), all resident in HBM.
     args.batches distinct batches (the steps rotate through them, so no step re-reads the
@@ -412,11 +514,14 @@ def bench_viterbi_only(args):
     def run_on(j, bi):
         with torch.cuda.stream(streams[j]):
             engs[j].viterbi(batches[bi][0], soft_off, params, outs[j][0], out_off, outs[j][1])
+        return streams[j]
 
     def step():
-        run_on(k["i"] % len(engs), k["i"] % nb)
+        st = run_on(k["i"] % len(engs), k["i"] % nb)
         k["i"] += 1
-    elapsed = _timed(step, args.steps, args.warmup)
+        return st
+    clock = StepClock(args.steps)
+    elapsed = _timed(step, args.steps, args.warmup, clock)
     match = True
     for bi in range(nb):                                      # every batch once more on every engine
         for j in range(len(engs)):
@@ -426,6 +531,22 @@ def bench_viterbi_only(args):
             match &= bool((o.reshape(n, stride)[:, :fl].cpu() == batches[bi][1]).all()) and bool((ob == 8 * fl).all())
     soft = batches[0][0]
     bits = n * fl * 8
+    line = {
+        "metric": "decoded Mbit/s, batched K=7 rate-1/2 Viterbi only (BASELINE config 2)",
+        "value": round(bits * args.steps / elapsed / 1e6, 1), "unit": "Mbit/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (random bits, 802.11a encoder, soft 7*bit+U[-2,2])",
+        "config": {"workload": f"config2: {n} frames x {fl} B, R=1/2, {ns} soft values each", "batches": nb},
+        "bit_exact_check": {"frames_equal_sent": match, "checked": f"every frame of all {nb} batches, every engine"},
+        "pipeline": (f"{len(engs)} batches in flight (engines on separate streams, steps in turn)" if len(engs) > 1
+                     else "1 batch in flight"),
+        "step_stats": clock.stats(),
+    }
+    for e in engs:
+        e.close()
+    if not cpu:
+        return line
     # CPU port (AVX-512 brick loop, identical to the oracle) on every allowed core, chunks of
     # the same frames for about --cpu-seconds
     threads, host = host_cpus()
@@ -442,24 +563,16 @@ def bench_viterbi_only(args):
         done += chunk
     cpu_dt = time.perf_counter() - t0
     vit = "AVX-512 vpermb" if O.lib().zp_fft64(None, None, 0) else "scalar"
-    print(json.dumps({
-        "metric": "decoded Mbit/s, batched K=7 rate-1/2 Viterbi only (BASELINE config 2)",
-        "value": round(bits * args.steps / elapsed / 1e6, 1), "unit": "Mbit/s", "n_gpus": 1,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-        "data": "synthetic (random bits, 802.11a encoder, soft 7*bit+U[-2,2])",
-        "config": {"workload": f"config2: {n} frames x {fl} B, R=1/2, {ns} soft values each", "batches": nb},
-        "bit_exact_check": {"frames_equal_sent": match, "checked": f"every frame of all {nb} batches, every engine"},
-        "pipeline": (f"{len(engs)} batches in flight (engines on separate streams, steps in turn)" if len(engs) > 1
-                     else "1 batch in flight"),
-        "cpu_baseline": {"value": round(done * fl * 8 / cpu_dt / 1e6, 2), "unit": "Mbit/s", "cores": threads,
-                         "kind": "port", "per_core": round(done * fl * 8 / cpu_dt / 1e6 / threads, 2), "host": host,
-                         "sample": f"{done} frames of the same batch, {cpu_dt:.1f} s wall on {threads} threads (CPU "
-                                   f"port: {vit} brick loop, identical to the oracle)"},
-    }), flush=True)
+    line["cpu_baseline"] = {"value": round(done * fl * 8 / cpu_dt / 1e6, 2), "unit": "Mbit/s", "cores": threads,
+                            "kind": "port", "per_core": round(done * fl * 8 / cpu_dt / 1e6 / threads, 2), "host": host,
+                            "sample": f"{done} frames of the same batch, {cpu_dt:.1f} s wall on {threads} threads (CPU "
+                                      f"port: {vit} brick loop, identical to the oracle)"}
+    if emit:
+        print(json.dumps(line), flush=True)
+    return line
 
 
-def bench_mixed(args):
+def bench_mixed(args, emit=True, cpu=True):
     """BASELINE config 5: mixed MCS batches through the whole chain, every packet distinct
     (txgen.make_mixed_fast); args.batches distinct batches, the steps rotate through them.
     Every CRC-passing payload of every batch is checked against what was sent and a sample of
@@ -498,10 +611,12 @@ def bench_mixed(args):
         m = ms[bi]
         with torch.cuda.stream(streams[j]):
             engs[j].rx(m["sym"], m["sym_off"], m["nsym"], S, outs[j][0], outs[j][1])
+        return streams[j]
 
     def step():
-        run_on(k["i"] % len(engs), k["i"] % nb)
+        st = run_on(k["i"] % len(engs), k["i"] % nb)
         k["i"] += 1
+        return st
 
     for _ in range(args.warmup):
         step()
@@ -516,7 +631,8 @@ def bench_mixed(args):
     stage = eng.stage_ms()
     eng.enable_timing(False)
     first = k["i"]
-    elapsed = _timed(step, args.steps, 0)
+    clock = StepClock(args.steps)
+    elapsed = _timed(step, args.steps, 0, clock)
     timed_batches = [(first + i) % nb for i in range(args.steps)]
     single = None
     if len(engs) > 1:                                    # the same batches with engine 0 alone, for comparison
@@ -535,8 +651,8 @@ def bench_mixed(args):
             run_on(j, bi)
         torch.cuda.synchronize()
         outs_equal &= all(bool((o[0] == outs[0][0]).all()) and bool((o[1] == outs[0][1]).all()) for o in outs[1:])
-        inf = outs[0][1].cpu().numpy()
-        pay = outs[0][0].cpu().numpy()
+        inf = outs[0][1].cpu().numpy().copy()          # (a copy: on a CPU test stub .cpu() aliases)
+        pay = outs[0][0].cpu().numpy().copy()
         ok = inf[:, 4] == 1
         good &= all((pay[i, :len(m["payload"][i])] == m["payload"][i]).all() for i in range(n) if ok[i])
         crc_pass += int(ok.sum())
@@ -551,11 +667,13 @@ def bench_mixed(args):
     soff, sn = m0["sym_off"][:sample].cpu().numpy(), m0["nsym"][:sample].cpu().numpy()
     sym_s = m0["sym"][:int((soff + sn).max())].cpu().numpy()
     opay, res = O.rx_batch_time(sym_s, soff, sn, nthreads=threads)
-    cpu = cpu_baseline(m0, args.cpu_seconds)
+    cpu = cpu_baseline(m0, args.cpu_seconds) if cpu else None
     oracle_match = all(int(inf[i, 4]) == r["crc_ok"] and int(inf[i, 2]) == r["len"] and
                        (not r["crc_ok"] or (pay[i, :r["len"] - 4] == opay[i, :r["len"] - 4]).all())
                        for i, r in enumerate(res))
-    print(json.dumps({
+    for e in engs:
+        e.close()
+    line = {
         "metric": "decoded Mbit/s, mixed-MCS 802.11a RX chain (BASELINE config 5)",
         "value": round(bits * args.steps / elapsed / 1e6, 1), "unit": "Mbit/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -571,8 +689,12 @@ def bench_mixed(args):
                      f"mode {link})" if len(engs) > 1 else "1 batch in flight"),
         "value_one_engine": round(bits * args.steps / single / 1e6, 1) if single else None,
         "stage_ms": {k: round(v, 4) for k, v in stage.items()},
+        "step_stats": clock.stats(),
         "cpu_baseline": cpu,
-    }), flush=True)
+    }
+    if emit:
+        print(json.dumps(line), flush=True)
+    return line
 
 
 PCIE5_X16_GBS = 32e9 * 16 * 128 / 130 / 8 / 1e9      # 63.0 GB/s per direction (PCIe 5.0 x16)
@@ -650,8 +772,21 @@ def bench_e2e(args):
         torch.cuda.synchronize()
     h2d_gbs = 4 * sym_bytes / (ev[0].elapsed_time(ev[1]) * 1e-3) / 1e9
     d2h_gbs = 4 * d_pay.numel() / (ev[1].elapsed_time(ev[2]) * 1e-3) / 1e9
+    import ziria_amd as Z
     p_dt, p_ok = timed_calls(pin, "pinned")
+    Z.set_host_register(0)                              # pageable arrays staged through pinned slots
     g_dt, g_ok = timed_calls(page, "pageable")
+    # the same pageable arrays page-locked by the library on first use (mode 2: this process
+    # keeps them mapped until it leaves the mode), then copied in place on every later call
+    Z.set_host_register(2)
+    tr = time.perf_counter()
+    for j in range(nb):
+        call(page[j], *outs["pageable"])
+    reg_first = (time.perf_counter() - tr) / nb
+    reg_stats = Z.node_stats()
+    r_dt, r_ok = timed_calls(page, "pageable")
+    Z.set_host_register(1)                              # (releases them)
+    devices = Z.get_devices()
     bits = n * L * 8
     rate = lambda dt: round(bits * args.steps / dt / 1e6, 1)
     bound = bits / (sym_bytes / (h2d_gbs * 1e9)) / 1e6      # payload Mbit/s if the link ran flat out
@@ -665,16 +800,24 @@ def bench_e2e(args):
         "config": {"workload": f"config3: {n} packets x {L} B @ 54 Mbps, {S} symbols each, "
                                f"{sym_bytes / 1e6:.1f} MB of samples per batch in host memory",
                    "call": "__ext_wifi_rx_batch (synchronous: samples in, payload slots + info out)"},
+        "devices": {"shards": devices, "how": "every visible gfx950 device (zrx_get_devices); a call is split "
+                                              "into contiguous packet ranges, one host thread, context and PCIe "
+                                              "link per device"},
         "end_to_end": {"pinned_Mbps": rate(p_dt), "pageable_Mbps": rate(g_dt),
+                       "pageable_registered_Mbps": rate(r_dt),
+                       "pageable_registered_frac_of_pinned": round(rate(r_dt) / rate(p_dt), 3),
+                       "pageable_first_call_registering_ms": round(reg_first * 1e3, 3),
+                       "register_stats_after_first_calls": reg_stats,
                        "pinned_ms_per_batch": round(p_dt / args.steps * 1e3, 3),
                        "pageable_ms_per_batch": round(g_dt / args.steps * 1e3, 3),
+                       "pageable_registered_ms_per_batch": round(r_dt / args.steps * 1e3, 3),
                        "kernel_only_Mbps": rate(k_dt), "kernel_only_ms_per_batch": round(k_dt / args.steps * 1e3, 3)},
         "link": {"h2d_GBps": round(h2d_gbs, 1), "d2h_GBps": round(d2h_gbs, 1), "peak_GBps": round(PCIE5_X16_GBS, 1),
                  "h2d_frac": round(h2d_gbs / PCIE5_X16_GBS, 3),
                  "h2d_bound_Mbps": round(bound, 1), "pinned_frac_of_h2d_bound": round(rate(p_dt) / bound, 3),
                  "measured": "torch pinned->device copies of one batch's samples (x4), device->pinned of its "
                              "payload slots (x4), HIP events"},
-        "bit_exact_check": {"pinned": p_ok, "pageable": g_ok,
+        "bit_exact_check": {"pinned": p_ok, "pageable": g_ok, "pageable_registered": r_ok,
                             "checked": f"every packet of all {nb} batches: CRC pass and payload = sent"},
         "host": dict(host, threads_available=threads),
     }), flush=True)

@@ -82,7 +82,10 @@ void __ext_sora_fft64_batch(struct complex16* out, int outlen, struct complex16*
  * init(frame_len[i], code_rate[i], 256) followed by decode calls over all its soft values,
  * writing its bytes at out_bits[pkt_out_off[i] ..] (byte offsets; bytes are LSB-first bit
  * arrays).  pkt_soft_off has npkts+1 entries; every per-packet soft count must be a multiple
- * of 48.  Returns the number of packets decoded, or a negative ZRX_E* code. */
+ * of 48, and the frames' output ranges [pkt_out_off[i], +frame_len[i]) must not overlap
+ * (ZRX_EINVAL).  Only the bytes a frame decoded are written; the rest of its range and every
+ * byte between ranges keep the caller's contents.  Returns the number of packets decoded, or a
+ * negative ZRX_E* code. */
 int32_t __ext_viterbi_batch_decode(char* soft, int softlen, int32_t* pkt_soft_off, int n_off,
                                    int32_t* frame_len, int n_fl, int16_t* code_rate, int n_cr,
                                    unsigned char* out_bits, int out_len_bits,
@@ -92,8 +95,16 @@ int32_t __ext_viterbi_batch_decode(char* soft, int softlen, int32_t* pkt_soft_of
  * GetData: packet i = symbols [pkt_sym_off[i], pkt_sym_off[i+1]) of `sym` (64 complex16 per
  * CP-removed OFDM symbol; the first is the SIGNAL symbol).  Writes the descrambled payload
  * (len-4 bytes) of packet i at payload[i*4096 ..] and pkt_info[8*i ..] = {modulation,
- * coding, len, header_err, crc_ok, status, symbols_used, viterbi_bits}.
- * Returns the number of packets whose CRC passed, or a negative ZRX_E* code. */
+ * coding, len, header_err, crc_ok, status, symbols_used, viterbi_bits}.  Only the first len-4
+ * bytes of a slot are defined: the rest may be zeros or keep the caller's bytes (this call
+ * writes a slot only as far as the widest payload its packets' symbol counts allow).
+ * Returns the number of packets whose CRC passed, or a negative ZRX_E* code.
+ *
+ * Every batched call of Part 2 is split into contiguous packet ranges over the node's GPUs
+ * (zrx_set_devices: by default every visible gfx950 device), one host thread, context and
+ * PCIe link per GPU, each range's outputs written straight into the caller's arrays; no data
+ * moves between GPUs.  Calls are serialized (one at a time, like the reference's global
+ * decoder), and the caller's current HIP device is left as it was. */
 int32_t __ext_wifi_rx_batch(struct complex16* sym, int nsym_total, int32_t* pkt_sym_off, int n_off,
                             unsigned char* payload, int payload_len_bits,
                             int32_t* pkt_info, int n_info);
@@ -116,7 +127,8 @@ int32_t __ext_wifi_rx_eq_batch(struct complex16* sym, int nsym_total, int32_t* p
  * and PilotTrack.  payload / pkt_info as __ext_wifi_rx_batch; det[8*i ..] = {detected,
  * noSamples, shift, energy, noise, maxCorr (CCAParams, const.blk:51-57), samples consumed by
  * the detection, first data sample}.  Returns the number of captures with a detected
- * packet whose CRC passed. */
+ * packet whose CRC passed.  Only the first len-4 bytes of a
+ * payload slot are defined, as for __ext_wifi_rx_batch. */
 int32_t __ext_wifi_rx_stream_batch(struct complex16* samples, int nsamples, int32_t* cap_off, int n_off,
                                    int downsample, unsigned char* payload, int payload_len_bits,
                                    int32_t* pkt_info, int n_info, int32_t* det, int n_det);
@@ -145,6 +157,7 @@ extern "C" {
 #define ZRX_ENOMEM (-3)    /* workspace too small / allocation failed */
 #define ZRX_ENODEV (-4)    /* no gfx950 device */
 #define ZRX_EPLAN (-5)     /* the Viterbi plan dropped rows past its bound (zrx_plan_check) */
+#define ZRX_EINTERNAL (-6) /* an internal consistency check failed (a bug: reported, never silent) */
 
 /* packet status in pkt_info[5] */
 #define ZRX_PKT_OK 0
@@ -254,6 +267,41 @@ int zrx_cca_pattern(int16_t* pattern512);
 /* Host-side copy of the engine's integer trig tables (sinx, cosx: 65536 entries by
  * unsigned angle; atan2x: 256x256 by (u8)y, (u8)x), csrc/intalglutx.h.  No GPU needed. */
 int zrx_trig_tables(int16_t* sin65536, int16_t* cos65536, int16_t* atan65536);
+
+/* ---- The node behind the batched externals of Part 2 (no device buffers involved). */
+
+/* The logical shards a batched call is split over: n device ids (a device may repeat, giving
+ * it several shards, each with its own context, stream and host thread), or n = 0 for the
+ * default: the ZRX_DEVICES environment list ("0,1,2,3"), else every visible gfx950 device.
+ * A call is split into at most min(shards, max(1, input bytes / min_shard_bytes)) contiguous
+ * packet ranges of nearly equal input bytes (min_shard_bytes < 0: the default, 16 MiB; 0:
+ * always every shard).  Drops the previous shard contexts.  ZRX_ENODEV if a listed device is
+ * not a gfx950 device. */
+int zrx_set_devices(const int32_t* devices, int n, int64_t min_shard_bytes);
+/* The shard list in use (resolving the default): writes up to cap device ids and returns the
+ * number of shards, or a negative ZRX_E* code (ZRX_ENODEV without a gfx950 device). */
+int zrx_get_devices(int32_t* devices, int cap);
+/* stats8 = {shards the last batched call ran on, host-register mode, caller ranges the library
+ * holds page-locked, their bytes, registrations made, calls that found their arrays already
+ * registered, registrations that failed, min_shard_bytes}. */
+int zrx_node_stats(int64_t* stats8);
+/* Page-locking of the caller's host arrays, so their copies skip the pinned staging slots:
+ * 0 = never; 1 (default, or ZRX_HOST_REGISTER=1) = arrays in the main program's static
+ * storage (.data/.bss: where wplc puts a program's arrays; never unmapped), registered on first
+ * use and kept; 2 = also any other array of at least 256 KiB, on first use -- the caller keeps
+ * those arrays mapped until it sets mode 0 or 1, which releases them (a page-lock must not
+ * outlive its memory).  Memory the caller pinned itself is always used in place. */
+int zrx_set_host_register(int mode);
+/* The split rule of zrx_set_devices on its own (host only, no GPU): packet i weighs
+ * prefix[i+1] - prefix[i] (np+1 non-decreasing entries); writes cut[0..k] (room for
+ * nshards+1) and returns k, the number of ranges [cut[j], cut[j+1]). */
+int zrx_shard_split(const int64_t* prefix, int np, int nshards, int64_t min_bytes, int32_t* cut);
+/* Host-only check of the shard runner (no GPU): splits as zrx_shard_split, runs one thread per
+ * range writing owner[i] = range index for its packets and merges their counts as a batched
+ * call does; the range fail_shard (or none, -1) returns ZRX_EINTERNAL instead.  Returns np,
+ * or the first failing range's code. */
+int zrx_shard_selftest(const int64_t* prefix, int np, int nshards, int64_t min_bytes, int32_t* owner,
+                       int fail_shard);
 
 /* Version / build string. */
 const char* zrx_version(void);

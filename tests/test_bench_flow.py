@@ -40,6 +40,20 @@ HARNESS = textwrap.dedent("""
     torch.cuda.Stream = Stream
     torch.cuda.current_stream = lambda *a, **k: "current"
     torch.cuda.stream = lambda s: contextlib.nullcontext()
+    torch.cuda.empty_cache = lambda *a, **k: None
+
+    class Event:                                  # (host clock in place of a HIP event)
+        def __init__(self, **k):
+            self.t = 0.0
+        def record(self, stream=None):
+            import time
+            self.t = time.perf_counter()
+        def elapsed_time(self, other):
+            return (other.t - self.t) * 1e3
+
+    torch.cuda.Event = Event
+    torch.cuda.get_device_properties = lambda d: types.SimpleNamespace(pci_domain_id=0, pci_bus_id=0x11 + int(
+        os.environ.get("RANK", "0")), pci_device_id=0, name="stub")
     bench.torch = types.SimpleNamespace(**{k: getattr(torch, k) for k in dir(torch) if not k.startswith("__")})
     bench.torch.device = lambda *a, **k: cpu
     init = dist.init_process_group
@@ -113,7 +127,7 @@ def _run(tmp_path, args):
 
 
 @pytest.mark.parametrize("args,k,w", [
-    (["--npkts", "24", "--steps", "4", "--warmup", "2", "--no-cpu"], 4, 2),
+    (["--npkts", "24", "--steps", "4", "--warmup", "2", "--no-cpu", "--no-sub"], 4, 2),
     (["--config", "5", "--npkts", "40", "--steps", "3", "--warmup", "1", "--cpu-seconds", "0.2", "--pipeline", "2"], 3, 1),
 ])
 def test_bench_pipelined_flow(oracle, tmp_path, args, k, w):
@@ -176,6 +190,11 @@ def test_bench_gpus2_spawns_two_ranks(oracle, tmp_path):
     assert b["packets"] == 2 * 24 and b["crc_pass"] == 2 * 24 and b["payload_match"] is True
     assert b["mismatched_packets"] == 0
     assert line["cpu_baseline"] is None and "N = 1" in line["cpu_baseline_note"]
+    # every rank's device and PCI address, and its own time over the timed region
+    assert [d["rank"] for d in line["devices"]] == [0, 1]
+    assert [d["pci"] for d in line["devices"]] == ["0000:11:00.0", "0000:12:00.0"]
+    assert all(d["elapsed_s"] > 0 for d in line["devices"])
+    assert "sub_results" not in line
     for r in (0, 1):
         assert any(e[0] == "rx" for e in logs[r])
     # the same run also decodes config 4 as SURVEY §8(d) defines it: npkts packets in all,
@@ -200,8 +219,31 @@ def test_bench_share_gpu_two_ranks(oracle, tmp_path):
 def test_bench_one_engine_flow(oracle, tmp_path):
     """--pipeline 1 (auto's choice at 8192 packets per GPU and above): one engine, no link,
     the timed steps and the verification all on engine 0."""
-    line, logs = _run(tmp_path, ["--npkts", "24", "--steps", "3", "--warmup", "1", "--no-cpu", "--pipeline", "1"])
+    line, logs = _run(tmp_path, ["--npkts", "24", "--steps", "3", "--warmup", "1", "--no-cpu", "--pipeline", "1",
+                                 "--no-sub"])
     log = logs[0]
     assert "1 batch in flight" in line["config"]["pipeline"]
     assert not any(e[0] == "link" for e in log) and all(e[1] == 0 for e in log if e[0] == "rx")
     assert line["bit_exact_check"]["payload_match"] is True and line["value_one_engine"] > 0
+
+
+def test_bench_default_line_carries_sub_results(oracle, tmp_path):
+    """The default one-GPU line: the headline plus configs 2 and 5 and the two config-4 shard
+    sizes as sub-results, each with its own bit-exact check, ms_per_step and per-step times
+    (npkts 32 here: shards of 4 and 8 packets)."""
+    line, logs = _run(tmp_path, ["--npkts", "32", "--payload", "200", "--steps", "2", "--warmup", "1", "--no-cpu"])
+    st = line["step_stats"]["gpu_step_ms"]
+    assert st["min"] <= st["median"] <= st["max"] and line["step_stats"]["host_issue_ms"]["max"] >= 0
+    assert line["devices"][0]["pci"] == "0000:11:00.0"
+    sub = line["sub_results"]
+    assert sorted(k for k in sub if k != "wall_s") == ["config2", "config5", "shard_4", "shard_8"]
+    assert sub["config2"]["bit_exact_check"]["frames_equal_sent"] is True
+    assert sub["config5"]["bit_exact_check"]["payload_match"] is True
+    assert sub["config5"]["bit_exact_check"]["oracle_sample_match"] is True
+    for k in ("shard_4", "shard_8"):
+        b = sub[k]["bit_exact_check"]
+        assert b["payload_match"] is True and b["mismatched_packets"] == 0 and b["packets"] == 2 * int(k[6:])
+    for k in ("config2", "config5", "shard_4", "shard_8"):
+        assert sub[k]["ms_per_step"] > 0 and sub[k]["value"] > 0
+        g = sub[k]["step_stats"]["gpu_step_ms"]
+        assert g["min"] <= g["median"] <= g["max"]

@@ -160,3 +160,34 @@ def test_caller_batched_rx_chain_fixture(caller, golden, tmp_path):
     for i in range(len(off)):
         e = g["mix_payload"][po[i]:po[i + 1]]
         assert (pay[i, :e.size] == e).all(), i
+
+
+@pytest.mark.gpu
+def test_caller_static_arrays_registered(caller, tmp_path):
+    """A wplc program keeps its arrays in static storage; __ext_wifi_rx_batch page-locks that
+    storage once (zrx_set_host_register mode 1, the default) and copies straight from and to
+    it on every later call, and a rewrite of the arrays between calls is seen by the next one.
+    2048 config-3 packets (30 MB of symbols) in the caller's .bss, three calls."""
+    import torch
+    from ziria_amd import txgen
+    b = txgen.make_batch(2048, seed=0x51A7, sigma=4.0, device="cuda")
+    S = b["max_nsym"]
+    (tmp_path / "sym.bin").write_bytes(np.ascontiguousarray(b["sym"].cpu().numpy()).tobytes())
+    (tmp_path / "m.txt").write_text(" ".join(str(i * S) for i in range(2049)))
+    del b["sym"]
+    torch.cuda.empty_cache()
+    _run(caller, "rxstatic", tmp_path / "sym.bin", tmp_path / "m.txt", tmp_path / "p.bin", tmp_path / "i.bin",
+         tmp_path / "log.txt")
+    calls = [ln.split() for ln in (tmp_path / "log.txt").read_text().splitlines()]
+    rc = [int(c[3]) for c in calls]
+    st = [[int(x) for x in c[7:15]] for c in calls]          # zrx_node_stats after each call
+    assert rc == [2048, 2048, 2047]
+    # mode 1; the static segment registered once (one range, >= the 38 MB of arrays), then hits
+    # stats: {shards, mode, ranges held, bytes held, registrations, hits, failures, min_shard_bytes}
+    assert st[0][1] == 1 and st[0][2] == 1 and st[0][3] >= 2048 * 57 * 256 + 2048 * 4096
+    assert st[0][4] == st[2][4] and st[2][2] == 1 and st[2][6] == 0
+    assert st[1][5] - st[0][5] == 3 and st[2][5] - st[1][5] == 3      # sym, payload, info: in place
+    pay = np.frombuffer((tmp_path / "p.bin").read_bytes(), np.uint8).reshape(-1, 4096)
+    assert (pay[:, :1500] == b["payload"]).all()
+    info = np.frombuffer((tmp_path / "i.bin").read_bytes(), np.int32).reshape(-1, 8)
+    assert info[5, 4] == 0 and (np.delete(info[:, 4], 5) == 1).all()

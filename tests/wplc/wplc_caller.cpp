@@ -19,6 +19,10 @@
 //   wplc_caller shift <in.bin> <shift> <out.bin>                       v_shift_right_complex16
 //   wplc_caller vbatch <soft.bin> <frame_len> <code_rate> <out.bin>    one-packet batch (GPU)
 //   wplc_caller rx <sym.bin> <manifest> <payload.bin> <info.bin>       __ext_wifi_rx_batch (GPU)
+//   wplc_caller rxstatic <sym.bin> <manifest> <payload.bin> <info.bin> <log.txt>
+//       the same from arrays in static storage, as wplc emits a program's arrays: three calls
+//       on the same arrays, the third after packet 5's SIGNAL symbol was wiped (GPU)
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -46,6 +50,14 @@ int32 __ext_viterbi_batch_decode(int8* soft, int __len_unused_11, int32* pkt_sof
                                  BitArrPtr out, int __len_unused_15, int32* pkt_out_off, int __len_unused_16);
 int32 __ext_wifi_rx_batch(complex16* sym, int __len_unused_17, int32* pkt_sym_off, int __len_unused_18,
                           BitArrPtr payload, int __len_unused_19, int32* pkt_info, int __len_unused_20);
+
+extern "C" int zrx_node_stats(long long* stats8);   // (libziria_rx.so's node counters; test only)
+
+// rxstatic's arrays: file-scope globals like the `calign` arrays of wplc's generated code
+static complex16 g_sym[2048 * 57 * 64];
+static unsigned char g_pay[2048 * 4096];
+static int32 g_info[2048 * 8];
+static int32 g_off[2049];
 
 static std::vector<char> slurp(const char* name) {
   std::vector<char> v;
@@ -134,6 +146,37 @@ int main(int argc, char** argv) {
     spill(argv[4], pay.data(), pay.size());
     spill(argv[5], info.data(), info.size() * sizeof(int32));
     return 0;
+  }
+  if (!std::strcmp(mode, "rxstatic") && argc == 7) {
+    std::vector<char> raw = slurp(argv[2]);
+    FILE* m = std::fopen(argv[3], "r");
+    if (!m) return 2;
+    int n_off = 0;
+    long v;
+    while (n_off < 2049 && std::fscanf(m, "%ld", &v) == 1) g_off[n_off++] = (int32)v;
+    std::fclose(m);
+    const int np = n_off - 1;
+    if (np < 6 || raw.size() > sizeof(g_sym) || (size_t)g_off[np] * 256 != raw.size()) return 2;
+    std::memcpy(g_sym, raw.data(), raw.size());
+    FILE* log = std::fopen(argv[6], "w");
+    if (!log) return 2;
+    int32 rc[3];
+    for (int k = 0; k < 3; k++) {
+      if (k == 2) std::memset(g_sym + (size_t)g_off[5] * 64, 0, 256);   // packet 5: SIGNAL symbol wiped
+      const auto t0 = std::chrono::steady_clock::now();
+      rc[k] = __ext_wifi_rx_batch(g_sym, g_off[np], g_off, n_off, g_pay, (int)sizeof(g_pay) * 8, g_info,
+                                  (int)(sizeof(g_info) / sizeof(int32)));
+      const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      long long st[8];
+      zrx_node_stats(st);
+      std::fprintf(log, "call %d rc %d ms %.3f stats", k, rc[k], ms);
+      for (long long x : st) std::fprintf(log, " %lld", x);
+      std::fprintf(log, " crc5 %d\n", g_info[8 * 5 + 4]);
+      if (k == 1) spill(argv[4], g_pay, (size_t)np * 4096);
+    }
+    spill(argv[5], g_info, (size_t)np * 8 * sizeof(int32));
+    std::fclose(log);
+    return rc[0] < 0 || rc[1] < 0 || rc[2] < 0 ? 1 : 0;
   }
   return 2;
 }

@@ -54,6 +54,12 @@ SIGNATURES = [
     ("zrx_tx_samples", C.c_int, [_P]),
     ("zrx_tx_preamble", C.c_int, [_P]),
     ("zrx_trig_tables", C.c_int, [_P, _P, _P]),
+    ("zrx_set_devices", C.c_int, [_P, C.c_int, C.c_int64]),
+    ("zrx_get_devices", C.c_int, [_P, C.c_int]),
+    ("zrx_node_stats", C.c_int, [_P]),
+    ("zrx_set_host_register", C.c_int, [C.c_int]),
+    ("zrx_shard_split", C.c_int, [_P, C.c_int, C.c_int, C.c_int64, _P]),
+    ("zrx_shard_selftest", C.c_int, [_P, C.c_int, C.c_int, C.c_int64, _P, C.c_int]),
     ("zrx_version", C.c_char_p, []),
 ]
 

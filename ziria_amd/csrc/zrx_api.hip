@@ -21,6 +21,7 @@
 #include "zrx_internal.h"
 #include "zrx_kernels.hip"
 #include "zrx_hostio.hpp"
+#include "zrx_shard.hpp"
 
 using namespace zrx;
 
@@ -44,6 +45,7 @@ struct zrx_ctx {
   int v3dbg = 0;                  // ZRX_V3DBG: k_viterbi3 timing-experiment variants (wrong output)
 #endif
   hipStream_t stream = nullptr;
+  bool owns_stream = false;       // a shard context of the batched externals: its own stream
   bool timing = false;
   // one set of 6 events per timed zrx_rx_dev launch since zrx_enable_timing (averaged by
   // zrx_get_timing), so stages are timed live inside a run of back-to-back launches
@@ -308,7 +310,7 @@ static int ensure_eq_tables(zrx_ctx* c) {
   std::vector<uint32_t> rot(65536);
   for (int r = 0; r < 65536; r++)     // build_coeff (PilotTrack.blk:28-50): (cos th, -sin th)
     rot[r] = (uint32_t)(uint16_t)cv[r] | ((uint32_t)(uint16_t)(int16_t)(-sv[r]) << 16);
-  ZRX_CHECK(hipSetDevice(c->device));
+  zrx_shard::DeviceGuard dg(c->device);   // (the caller's device is restored on return)
   ZRX_CHECK(hipMalloc(&c->eq_rot, 65536 * 4));
   ZRX_CHECK(hipMalloc(&c->eq_atan, 65536 * 2));
   ZRX_CHECK(hipMemcpy(c->eq_rot, rot.data(), 65536 * 4, hipMemcpyHostToDevice));
@@ -387,7 +389,7 @@ static int fftn_plans(zrx_ctx* c) {
   const std::vector<FftPlan>& plans = R.plans;
   const std::vector<uint32_t>& tw = R.tw;
   const std::vector<uint16_t>& pos = R.pos;
-  ZRX_CHECK(hipSetDevice(c->device));
+  zrx_shard::DeviceGuard dg(c->device);   // (the caller's device is restored on return)
   ZRX_CHECK(hipMalloc(&c->fft_plans, sizeof(FftPlan) * kFftSizes));
   ZRX_CHECK(hipMalloc(&c->fft_tw, tw.size() * 4));
   ZRX_CHECK(hipMalloc(&c->fft_pos, pos.size() * 2));
@@ -416,7 +418,7 @@ int zrx_create(zrx_ctx** out, int device, void* stream) {
   *out = nullptr;
   int rc = check_device(device);
   if (rc) return rc;
-  ZRX_CHECK(hipSetDevice(device));
+  zrx_shard::DeviceGuard dg(device);
   zrx_ctx* c = new zrx_ctx();
   c->device = device;
   ZRX_CHECK(hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device));
@@ -449,7 +451,7 @@ int zrx_create(zrx_ctx** out, int device, void* stream) {
 
 int zrx_destroy(zrx_ctx* c) {
   if (!c) return ZRX_OK;
-  (void)hipSetDevice(c->device);
+  zrx_shard::DeviceGuard dg(c->device);
   free_ws(c);
   (void)hipFree(c->eq_rot);
   (void)hipFree(c->eq_atan);
@@ -476,6 +478,7 @@ int zrx_destroy(zrx_ctx* c) {
     (void)hipEventDestroy(c->ev_fork);
     (void)hipEventDestroy(c->ev_join);
   }
+  if (c->owns_stream && c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return ZRX_OK;
 }
@@ -491,7 +494,7 @@ int zrx_pipeline_link(zrx_ctx* a, zrx_ctx* b, int mode) {
   // the link orders two streams of one device (events without a system fence, the low-
   // priority head stream beside the engine's own): both engines must be on it
   if (a->device != b->device) return ZRX_EINVAL;
-  ZRX_CHECK(hipSetDevice(a->device));
+  zrx_shard::DeviceGuard dg(a->device);
   for (zrx_ctx* c : {a, b}) {
     if (c->peer && c->peer != a && c->peer != b) { c->peer->peer = nullptr; c->peer->link_mode = 0; }
     // stream-to-stream on one device: no system-scope fence (which writes back the L2s)
@@ -544,7 +547,7 @@ int zrx_get_timing(zrx_ctx* c, float* ms5) {
 int zrx_reserve(zrx_ctx* c, int npkts, int max_nsym) {
   if (!c || npkts < 0 || max_nsym < 1) return ZRX_EINVAL;
   if (npkts <= c->cap_pkts && max_nsym <= c->cap_nsym) return ZRX_OK;
-  ZRX_CHECK(hipSetDevice(c->device));
+  zrx_shard::DeviceGuard dg(c->device);   // (the caller's device is restored on return)
   const int np = std::max(npkts, c->cap_pkts), ns = std::max(max_nsym, c->cap_nsym);
   free_ws(c);
   const int64_t stride = ((int64_t)std::max(ns - 1, 1) * 288 + 255) / 256 * 256;
@@ -801,7 +804,7 @@ int zrx_rx_stream_dev(zrx_ctx* c, const struct complex16* d_samples, const int64
   if (rc) return rc;
   rc = ensure_eq_tables(c);
   if (rc) return rc;
-  ZRX_CHECK(hipSetDevice(c->device));
+  zrx_shard::DeviceGuard dg(c->device);   // (the caller's device is restored on return)
   if (!c->fe_pattern) {
     uint32_t pat[256];
     make_cca_pattern(pat);
@@ -835,7 +838,7 @@ int zrx_tx_dev(zrx_ctx* c, const uint8_t* d_in, const int64_t* d_in_off, int npk
                const int64_t* d_out_off, int32_t* d_nsamp) {
   if (!c || npkts < 0 || (npkts > 0 && (!d_in || !d_in_off || !d_out || !d_out_off || !d_nsamp))) return ZRX_EINVAL;
   if (npkts == 0) return ZRX_OK;
-  ZRX_CHECK(hipSetDevice(c->device));
+  zrx_shard::DeviceGuard dg(c->device);   // (the caller's device is restored on return)
   if (!c->tx_preamble) {
     uint32_t pre[640];
     make_tx_preamble(pre);
@@ -885,19 +888,104 @@ int zrx_trig_tables(int16_t* sin65536, int16_t* cos65536, int16_t* atan65536) {
 
 // ------------------------------------------------------------------ batched externals (host arrays)
 // The per-call externals (Part 1 of ziria_rx.h) run on the host: zrx_host.cpp.  The batched
-// ones below stage host arrays through one default GPU context and launch the chain.
-static std::mutex g_mu;
-static zrx_ctx* g_ctx = nullptr;
+// ones below split every call over the node's logical shards (zrx_shard.hpp): contiguous
+// packet ranges, one engine context per shard on its own device, stream, copy streams and
+// host thread, each writing its packets' outputs straight into the caller's arrays.
+static std::mutex g_mu;                  // one batched call at a time (the reference's decoder is global too)
 
-// The default context (device of the calling thread), created on first use; nullptr without
-// a gfx950 device: the batched externals then return ZRX_ENODEV (they have no CPU path).
-static zrx_ctx* default_ctx() {
-  if (g_ctx) return g_ctx;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-  if (zrx_create(&g_ctx, dev, nullptr) != ZRX_OK) g_ctx = nullptr;
-  return g_ctx;
+namespace {
+struct Node {
+  std::vector<int> want;                 // zrx_set_devices (empty: ZRX_DEVICES, else every gfx950 device)
+  int64_t min_shard_bytes = zrx_shard::kMinShardBytes;
+  bool resolved = false;
+  std::vector<int> dev;                  // device of each logical shard
+  std::vector<zrx_ctx*> ctx;             // its engine context, created on first use
+  zrx_io::Pool* pool = nullptr;          // the shards' host threads (shards - 1 workers + the caller)
+  zrx_shard::HostRegistry reg;           // caller arrays the library page-locked
+  int last_shards = 0;                   // shards the last call ran on
+};
+Node g_node;
+}  // namespace
+
+static bool is_gfx950(int device) {
+  hipDeviceProp_t prop;
+  return hipGetDeviceProperties(&prop, device) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
 }
+
+// Drops every shard context (the calls are synchronous: nothing of theirs is in flight).
+static void node_reset() {
+  for (size_t k = 0; k < g_node.ctx.size(); k++)
+    if (g_node.ctx[k]) zrx_destroy(g_node.ctx[k]);
+  g_node.ctx.clear();
+  g_node.dev.clear();
+  delete g_node.pool;
+  g_node.pool = nullptr;
+  g_node.resolved = false;
+}
+
+// The logical shards: zrx_set_devices' list, else ZRX_DEVICES, else every visible gfx950
+// device.  ZRX_ENODEV without one (the batched externals have no CPU path).
+static int node_resolve() {
+  if (g_node.resolved) return ZRX_OK;
+  std::vector<int> d = g_node.want;
+  if (d.empty()) d = zrx_shard::parse_devices(std::getenv("ZRX_DEVICES"));
+  if (d.empty()) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+      (void)hipGetLastError();
+      n = 0;
+    }
+    for (int i = 0; i < n; i++)
+      if (is_gfx950(i)) d.push_back(i);
+  }
+  if (d.empty()) {
+    std::fprintf(stderr, "ziria_rx: no gfx950 device: the batched externals run on the GPU (no CPU path)\n");
+    return ZRX_ENODEV;
+  }
+  for (int x : d)
+    if (check_device(x) != ZRX_OK) return ZRX_ENODEV;
+  g_node.dev = d;
+  g_node.ctx.assign(d.size(), nullptr);
+  g_node.pool = new zrx_io::Pool((int)d.size());
+  g_node.resolved = true;
+  return ZRX_OK;
+}
+
+// Shard k's context (own non-blocking stream on its device), created on first use.  Distinct
+// shards are created from distinct threads: each touches only its own slot.
+static zrx_ctx* node_ctx(int k) {
+  if (g_node.ctx[(size_t)k]) return g_node.ctx[(size_t)k];
+  const int dev = g_node.dev[(size_t)k];
+  zrx_shard::DeviceGuard dg(dev);
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  zrx_ctx* c = nullptr;
+  if (zrx_create(&c, dev, s) != ZRX_OK) {
+    (void)hipStreamDestroy(s);
+    return nullptr;
+  }
+  c->owns_stream = true;
+  return g_node.ctx[(size_t)k] = c;
+}
+
+// Splits a call of np packets (weight prefix: the input bytes before packet i) over the
+// shards and runs body(ctx, p0, p1) for each range on its shard's device; merged as
+// zrx_shard::run: the first error, else the sum of the bodies' counts.
+template <class Prefix, class Body>
+static int node_run(int np, Prefix prefix, Body&& body) {
+  int rc = node_resolve();
+  if (rc) return rc;
+  const std::vector<int> cut = zrx_shard::split(np, prefix, (int)g_node.dev.size(), g_node.min_shard_bytes);
+  g_node.last_shards = (int)cut.size() - 1;
+  return zrx_shard::run(g_node.pool, cut, [&](int k, int p0, int p1) -> int {
+    zrx_ctx* c = node_ctx(k);
+    if (!c) return ZRX_ENODEV;
+    zrx_shard::DeviceGuard dg(c->device);
+    return body(c, p0, p1);
+  });
+}
+
+static bool registered(const void* p, size_t n) { return g_node.reg.ensure(p, n, zrx_io::is_pinned); }
 
 static void* staging(zrx_ctx* c, size_t bytes) {
   if (bytes > c->small_cap) {
@@ -924,35 +1012,17 @@ static void* pinned_mapped(size_t bytes, void** dev) {
     std::fprintf(stderr, "ziria_rx: %s (%s:%d)\n", msg, __FILE__, __LINE__); \
     std::abort();                                                        \
   } while (0)
-#define ZRX_OR_DIE(call) \
-  do { if ((call) != hipSuccess) ZRX_DIE(#call); } while (0)
 
 namespace zrx_batch {
 
-// nsym independent FFT64s (no return value to carry an error: fails loudly without a GPU)
-void sora_fft64_batch(struct complex16* out, int outlen, struct complex16* in, int inlen) {
-  if (inlen <= 0 || inlen % 64 || outlen < inlen) {
-    std::fprintf(stderr, "ziria_rx: __ext_sora_fft64_batch needs inlen = 64*k and outlen >= inlen\n");
-    return;
-  }
-  std::lock_guard<std::mutex> lk(g_mu);
-  zrx_ctx* c = default_ctx();
-  if (!c) ZRX_DIE("no gfx950 device: the batched externals run on the GPU");
-  const size_t bytes = (size_t)inlen * 4;
-  uint8_t* d = (uint8_t*)staging(c, 2 * bytes);
-  if (!d) ZRX_DIE("staging allocation failed");
-  ZRX_OR_DIE(hipMemcpyAsync(d, in, bytes, hipMemcpyHostToDevice, c->stream));
-  if (zrx_fft64_dev(c, (const complex16*)d, (complex16*)(d + bytes), inlen / 64) != ZRX_OK) ZRX_DIE("fft launch");
-  ZRX_OR_DIE(hipMemcpyAsync(out, d + bytes, bytes, hipMemcpyDeviceToHost, c->stream));
-  ZRX_OR_DIE(hipStreamSynchronize(c->stream));
-}
-
-
-// The host pipelines' per-context state (zrx_hostio.hpp), created on first use.
+// The host pipelines' per-context state (zrx_hostio.hpp), created on first use; its copy pool
+// gets this shard's share of the host threads.
 static zrx_io::HostIO* host_io(zrx_ctx* c) {
   if (c->hio) return c->hio;
   auto* io = new zrx_io::HostIO();
-  if (io->init(c->device) != hipSuccess) {
+  const unsigned hc = std::max(1u, std::thread::hardware_concurrency());
+  const int share = (int)std::min<unsigned>(8u, std::max(1u, hc / 2 / (unsigned)std::max<size_t>(1, g_node.dev.size())));
+  if (io->init(c->device, share) != hipSuccess) {
     std::fprintf(stderr, "ziria_rx: copy streams / events for the host pipeline could not be created\n");
     delete io;
     return nullptr;
@@ -981,52 +1051,82 @@ static int plan_flags_ok(const zrx_io::HostIO* io, int nch) {
   return ZRX_OK;
 }
 
-// Packet i decodes soft[so[i] .. so[i+1]) and its bytes land at out_bits[pkt_out_off[i] ..].
-// The frames are decoded into a packed device buffer (frame i at the prefix of frame_len) and
-// only the bytes each frame produced (out_bits_count / 8: the brick emits whole bytes, window
-// by window) are scattered into the caller's array, whose other bytes stay as they were; so
-// the caller's output array is never uploaded.  Soft values go up in chunks (zrx_hostio.hpp).
-int32_t viterbi_batch_decode(const char* soft, int softlen, const int32_t* pkt_soft_off, int n_off,
-                             const int32_t* frame_len, int n_fl, const int16_t* code_rate, int n_cr,
-                             unsigned char* out_bits, int out_len_bits, const int32_t* pkt_out_off, int n_oo) {
-  const int np = n_off - 1;
-  if (np < 0 || n_fl < np || n_cr < np || n_oo < np || softlen < 0 || out_len_bits < 0) return ZRX_EINVAL;
-  if (np == 0) return 0;
-  const int64_t out_bytes = out_len_bits / 8;
+// ---- FFT64 batch: symbols [q0, q1) of one shard
+static int fft64_range(zrx_ctx* c, struct complex16* out, const struct complex16* in, int q0, int q1) {
+  const size_t bytes = (size_t)(q1 - q0) * 256;
+  uint8_t* d = (uint8_t*)staging(c, 2 * bytes);
+  if (!d) return ZRX_ENOMEM;
+  ZRX_CHECK(hipMemcpyAsync(d, (const uint8_t*)in + (size_t)q0 * 256, bytes, hipMemcpyHostToDevice, c->stream));
+  const int rc = zrx_fft64_dev(c, (const complex16*)d, (complex16*)(d + bytes), q1 - q0);
+  if (rc) return rc;
+  ZRX_CHECK(hipMemcpyAsync((uint8_t*)out + (size_t)q0 * 256, d + bytes, bytes, hipMemcpyDeviceToHost, c->stream));
+  ZRX_CHECK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+// nsym independent FFT64s (no return value to carry an error: fails loudly without a GPU)
+void sora_fft64_batch(struct complex16* out, int outlen, struct complex16* in, int inlen) {
+  if (inlen <= 0 || inlen % 64 || outlen < inlen) {
+    std::fprintf(stderr, "ziria_rx: __ext_sora_fft64_batch needs inlen = 64*k and outlen >= inlen\n");
+    return;
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  const int rc = node_run(inlen / 64, [](int i) { return (int64_t)i * 256; },
+                          [&](zrx_ctx* c, int q0, int q1) { return fft64_range(c, out, in, q0, q1); });
+  if (rc == ZRX_ENODEV) ZRX_DIE("no gfx950 device: the batched externals run on the GPU");
+  if (rc < 0) ZRX_DIE("__ext_sora_fft64_batch failed");
+}
+
+// ---- Viterbi batch
+struct VitCall {
+  const char* soft;
+  const int32_t* soft_off;                 // n + 1 (validated: non-decreasing, within softlen)
+  const int32_t* frame_len;
+  const int16_t* code_rate;
+  unsigned char* out;
+  const int32_t* out_off;
+  bool pin_in;
+};
+
+// Packets [q0, q1) of one shard: frame i decodes soft[soft_off[i] .. soft_off[i+1]) and its
+// bytes land at out[out_off[i] ..].  The frames are decoded into a packed device buffer (frame
+// i at the prefix of frame_len) and only the bytes each frame produced (out_bits_count / 8: the
+// brick emits whole bytes, window by window) are scattered into the caller's array, whose other
+// bytes stay as they were; so the caller's output array is never uploaded.  The shard's soft
+// values go up in chunks (zrx_hostio.hpp) into a device copy of just its range.
+static int vit_range(zrx_ctx* c, const VitCall& a, int q0, int q1) {
+  const int np = q1 - q0;
+  if (np <= 0) return 0;
+  const int64_t base = a.soft_off[q0];
   std::vector<int32_t> params(4 * (size_t)np);
   std::vector<int64_t> soff(np), coff(np + 1);
   coff[0] = 0;
   for (int i = 0; i < np; i++) {
-    const int32_t n = pkt_soft_off[i + 1] - pkt_soft_off[i];
-    const int cr = code_rate[i];
-    if (cr < 0 || cr > 2 || n < 0 || n % 48 || pkt_soft_off[i] < 0 || pkt_soft_off[i + 1] > softlen ||
-        frame_len[i] < 0 || frame_len[i] > 4990 || pkt_out_off[i] < 0 || pkt_out_off[i] + (int64_t)frame_len[i] > out_bytes)
-      return ZRX_EINVAL;
-    params[4 * i] = frame_len[i]; params[4 * i + 1] = cr; params[4 * i + 2] = n; params[4 * i + 3] = 0;
-    soff[i] = pkt_soft_off[i];
-    coff[i + 1] = coff[i] + frame_len[i];
+    const int g = q0 + i;
+    params[4 * i] = a.frame_len[g];
+    params[4 * i + 1] = a.code_rate[g];
+    params[4 * i + 2] = a.soft_off[g + 1] - a.soft_off[g];
+    params[4 * i + 3] = 0;
+    soff[i] = a.soft_off[g] - base;
+    coff[i + 1] = coff[i] + a.frame_len[g];
   }
-  const std::vector<int> cut = zrx_io::chunk_cuts(
-      np, [&](int i) { return (size_t)(pkt_soft_off[i + 1] - pkt_soft_off[i]); },
-      (size_t)(pkt_soft_off[np] - pkt_soft_off[0]));
+  const auto sof = [&](int i) { return (size_t)(a.soft_off[q0 + i] - base); };   // local soft offset of packet i
+  const std::vector<int> cut = zrx_io::chunk_cuts(np, [&](int i) { return sof(i + 1) - sof(i); }, sof(np));
   const int nch = (int)cut.size() - 1;
   int maxn = 0;
   size_t in_max = 0, out_max = 0;
   for (int j = 0; j < nch; j++) {
     const int n = cut[j + 1] - cut[j];
     maxn = std::max(maxn, n);
-    in_max = std::max(in_max, (size_t)(pkt_soft_off[cut[j + 1]] - pkt_soft_off[cut[j]]));
+    in_max = std::max(in_max, sof(cut[j + 1]) - sof(cut[j]));
     out_max = std::max(out_max, (size_t)n * 4 + (size_t)(coff[cut[j + 1]] - coff[cut[j]]));
   }
-  std::lock_guard<std::mutex> lk(g_mu);
-  zrx_ctx* c = default_ctx();
-  if (!c) return ZRX_ENODEV;
   int rc = zrx_reserve(c, maxn, 1);                  // room for the row plan of k_pkt_plan
   if (rc) return rc;
   zrx_io::HostIO* io = host_io(c);
   if (!io) return ZRX_EHIP;
   const auto al = [](size_t b) { return (b + 255) / 256 * 256; };
-  const size_t s_soft = al((size_t)softlen), s_par = al((size_t)np * 16), s_off = al((size_t)np * 8);
+  const size_t s_soft = al(sof(np)), s_par = al((size_t)np * 16), s_off = al((size_t)np * 8);
   const size_t s_out = al((size_t)coff[np]);
   uint8_t* d = (uint8_t*)staging(c, s_soft + s_par + 2 * s_off + s_out + al((size_t)np * 4));
   if (!d) return ZRX_ENOMEM;
@@ -1036,8 +1136,8 @@ int32_t viterbi_batch_decode(const char* soft, int softlen, const int32_t* pkt_s
   int64_t* d_coff = (int64_t*)((uint8_t*)d_soff + s_off);
   uint8_t* d_out = (uint8_t*)d_coff + s_off;
   int32_t* d_bits = (int32_t*)(d_out + s_out);
-  const bool pin_in = zrx_io::is_pinned(soft + pkt_soft_off[0], (size_t)(pkt_soft_off[np] - pkt_soft_off[0]));
-  if ((!pin_in && io->reserve_in(in_max) != hipSuccess) || io->reserve_out(out_max) != hipSuccess ||
+  const char* hsoft = a.soft + base;
+  if ((!a.pin_in && io->reserve_in(in_max) != hipSuccess) || io->reserve_out(out_max) != hipSuccess ||
       io->reserve_flags(nch) != hipSuccess)
     return ZRX_ENOMEM;
   auto run = [&]() -> int {
@@ -1052,17 +1152,17 @@ int32_t viterbi_batch_decode(const char* soft, int softlen, const int32_t* pkt_s
       const int32_t* bits = (const int32_t*)(bytes + (size_t)(coff[p1] - coff[p0]));
       io->pool->run((p1 - p0 + 255) / 256, [&](int t) {
         for (int i = p0 + 256 * t; i < std::min(p1, p0 + 256 * (t + 1)); i++) {
-          const int nb = std::min<int>(frame_len[i], (std::max(bits[i - p0], 0) + 7) / 8);
-          std::memcpy(out_bits + pkt_out_off[i], bytes + (coff[i] - coff[p0]), (size_t)nb);
+          const int nb = std::min<int>(a.frame_len[q0 + i], (std::max(bits[i - p0], 0) + 7) / 8);
+          std::memcpy(a.out + a.out_off[q0 + i], bytes + (coff[i] - coff[p0]), (size_t)nb);
         }
       });
       return ZRX_OK;
     };
     for (int j = 0; j < nch; j++) {
       const int slot = j & 1, p0 = cut[j], p1 = cut[j + 1], n = p1 - p0;
-      const size_t s0 = (size_t)pkt_soft_off[p0], sb = (size_t)(pkt_soft_off[p1] - pkt_soft_off[p0]);
-      const char* src = soft + s0;
-      if (!pin_in) {
+      const size_t s0 = sof(p0), sb = sof(p1) - sof(p0);
+      const char* src = hsoft + s0;
+      if (!a.pin_in) {
         ZRX_CHECK(hipEventSynchronize(io->up_done[slot]));   // the slot's last upload is done
         zrx_io::par_copy(*io->pool, io->in[slot], src, sb);
         src = (const char*)io->in[slot];
@@ -1094,33 +1194,76 @@ int32_t viterbi_batch_decode(const char* soft, int softlen, const int32_t* pkt_s
   return rc ? rc : np;
 }
 
-
-// receiveBits over host packets; chan (64 coefficients per packet, chan_len >= 64 npkts) adds
-// ChannelEqualization + PilotTrack.  Chunks of whole packets are uploaded, decoded and
-// downloaded in a pipeline (zrx_hostio.hpp); a chunk's payload slots come back `cw` bytes
-// wide: the most a packet of that chunk can carry (LENGTH - 4 <= 27 x data symbols - 6 at
-// 54 Mbps, 216 bits a symbol for LENGTH + 2 decoded bytes; <= 2044 since LENGTH <= 2048),
-// which k_descramble_crc writes in whole dwords after the chunk's memset zeroes them.
-int32_t wifi_rx_batch(struct complex16* sym, int nsym_total, const int32_t* pkt_sym_off, int n_off,
-                      const struct complex16* chan, int chan_len, unsigned char* payload, int payload_len_bits,
-                      int32_t* pkt_info, int n_info) {
+int32_t viterbi_batch_decode(const char* soft, int softlen, const int32_t* pkt_soft_off, int n_off,
+                             const int32_t* frame_len, int n_fl, const int16_t* code_rate, int n_cr,
+                             unsigned char* out_bits, int out_len_bits, const int32_t* pkt_out_off, int n_oo) {
   const int np = n_off - 1;
-  if (np < 0 || nsym_total < 0 || n_info < 8 * np || (int64_t)payload_len_bits / 8 < (int64_t)np * kPayloadStride)
-    return ZRX_EINVAL;
-  if (chan && chan_len < 64 * (int64_t)np) return ZRX_EINVAL;
+  if (np < 0 || n_fl < np || n_cr < np || n_oo < np || softlen < 0 || out_len_bits < 0) return ZRX_EINVAL;
   if (np == 0) return 0;
+  const int64_t out_bytes = out_len_bits / 8;
+  for (int i = 0; i < np; i++) {
+    const int32_t n = pkt_soft_off[i + 1] - pkt_soft_off[i];
+    const int cr = code_rate[i];
+    if (cr < 0 || cr > 2 || n < 0 || n % 48 || pkt_soft_off[i] < 0 || pkt_soft_off[i + 1] > softlen ||
+        frame_len[i] < 0 || frame_len[i] > 4990 || pkt_out_off[i] < 0 || pkt_out_off[i] + (int64_t)frame_len[i] > out_bytes)
+      return ZRX_EINVAL;
+  }
+  // the frames' output ranges must not overlap: the shards (and each shard's copy threads)
+  // write them concurrently
+  {
+    std::vector<int> ord;
+    ord.reserve(np);
+    for (int i = 0; i < np; i++)
+      if (frame_len[i] > 0) ord.push_back(i);
+    std::sort(ord.begin(), ord.end(), [&](int x, int y) { return pkt_out_off[x] < pkt_out_off[y]; });
+    for (size_t k = 1; k < ord.size(); k++)
+      if ((int64_t)pkt_out_off[ord[k - 1]] + frame_len[ord[k - 1]] > pkt_out_off[ord[k]]) {
+        std::fprintf(stderr, "ziria_rx: __ext_viterbi_batch_decode: output ranges of frames %d and %d overlap\n",
+                     ord[k - 1], ord[k]);
+        return ZRX_EINVAL;
+      }
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  const int rc0 = node_resolve();
+  if (rc0) return rc0;
+  VitCall a{soft, pkt_soft_off, frame_len, code_rate, out_bits, pkt_out_off, false};
+  a.pin_in = registered(soft + pkt_soft_off[0], (size_t)(pkt_soft_off[np] - pkt_soft_off[0]));
+  return node_run(np, [&](int i) { return (int64_t)pkt_soft_off[i]; },
+                  [&](zrx_ctx* c, int q0, int q1) { return vit_range(c, a, q0, q1); });
+}
+
+// ---- receiveBits batch
+struct RxCall {
+  const uint8_t* sym;                      // 256 B per symbol
+  const int32_t* sym_off;                  // n + 1 (validated)
+  const uint8_t* chan;                     // 256 B per packet, or nullptr
+  unsigned char* payload;                  // kPayloadStride B per packet
+  int32_t* info;                           // 8 per packet
+  bool pin_in, pin_out;
+};
+
+// Packets [q0, q1) of one shard: chunks of whole packets are uploaded, decoded and downloaded
+// in a pipeline (zrx_hostio.hpp), the device holding only this shard's symbols.  A chunk's
+// payload slots come back `cw` bytes wide: the most a packet of that chunk can carry (LENGTH -
+// 4 <= 27 x data symbols - 6 at 54 Mbps, 216 bits a symbol for LENGTH + 2 decoded bytes;
+// <= 2044 since LENGTH <= 2048), which k_descramble_crc writes in whole dwords after the
+// chunk's memset zeroes them; a slot's bytes past cw keep the caller's contents.
+static int rx_range(zrx_ctx* c, const RxCall& a, int q0, int q1) {
+  const int np = q1 - q0;
+  if (np <= 0) return 0;
+  const int64_t base = a.sym_off[q0];
   std::vector<int64_t> off(np);
   std::vector<int32_t> ns(np);
   int max_ns = 1;
   for (int i = 0; i < np; i++) {
-    if (pkt_sym_off[i] < 0 || pkt_sym_off[i + 1] < pkt_sym_off[i] || pkt_sym_off[i + 1] > nsym_total) return ZRX_EINVAL;
-    off[i] = pkt_sym_off[i];
-    ns[i] = pkt_sym_off[i + 1] - pkt_sym_off[i];
+    off[i] = a.sym_off[q0 + i] - base;
+    ns[i] = a.sym_off[q0 + i + 1] - a.sym_off[q0 + i];
     max_ns = std::max(max_ns, ns[i]);
   }
-  const size_t cb = chan ? 256 : 0;                  // channel bytes per packet
+  const size_t cb = a.chan ? 256 : 0;                // channel bytes per packet
+  const int64_t nsym = a.sym_off[q1] - base;
   const std::vector<int> cut = zrx_io::chunk_cuts(np, [&](int i) { return (size_t)ns[i] * 256 + cb; },
-                                                   (size_t)(pkt_sym_off[np] - pkt_sym_off[0]) * 256 + cb * np);
+                                                   (size_t)nsym * 256 + cb * np);
   const int nch = (int)cut.size() - 1;
   std::vector<int> cmax(nch, 1), cw(nch, 0);
   int maxn = 0;
@@ -1130,18 +1273,16 @@ int32_t wifi_rx_batch(struct complex16* sym, int nsym_total, const int32_t* pkt_
     for (int i = cut[j]; i < cut[j + 1]; i++) cmax[j] = std::max(cmax[j], ns[i]);
     cw[j] = (std::min(2044, std::max(27 * (cmax[j] - 1) - 6, 0)) + 3) & ~3;
     maxn = std::max(maxn, n);
-    in_max = std::max(in_max, (size_t)(pkt_sym_off[cut[j + 1]] - pkt_sym_off[cut[j]]) * 256 + cb * n);
+    const int64_t s0 = j + 1 < nch ? off[cut[j + 1]] : nsym;
+    in_max = std::max(in_max, (size_t)(s0 - off[cut[j]]) * 256 + cb * n);
     out_max = std::max(out_max, (size_t)n * 32 + (size_t)n * cw[j]);
   }
-  std::lock_guard<std::mutex> lk(g_mu);
-  zrx_ctx* c = default_ctx();
-  if (!c) return ZRX_ENODEV;
   int rc = zrx_reserve(c, maxn, max_ns);
   if (rc) return rc;
   zrx_io::HostIO* io = host_io(c);
   if (!io) return ZRX_EHIP;
   const auto al = [](size_t b) { return (b + 255) / 256 * 256; };
-  const size_t s_sym = al((size_t)pkt_sym_off[np] * 256) + 256;
+  const size_t s_sym = al((size_t)nsym * 256) + 256;
   const size_t s_off = al((size_t)np * 8), s_ns = al((size_t)np * 4);
   const size_t s_pay = (size_t)np * kPayloadStride, s_info = al((size_t)np * 32);
   const size_t s_chan = (size_t)np * cb;
@@ -1153,13 +1294,11 @@ int32_t wifi_rx_batch(struct complex16* sym, int nsym_total, const int32_t* pkt_
   uint8_t* d_pay = (uint8_t*)d_ns + s_ns;
   int32_t* d_info = (int32_t*)(d_pay + s_pay);
   uint8_t* d_chan = (uint8_t*)d_info + s_info;
-  const uint8_t* hs = (const uint8_t*)sym;
-  const bool pin_in = zrx_io::is_pinned(hs + (size_t)pkt_sym_off[0] * 256,
-                                        (size_t)(pkt_sym_off[np] - pkt_sym_off[0]) * 256) &&
-                      (!chan || zrx_io::is_pinned(chan, (size_t)np * 256));
-  const bool pin_out = zrx_io::is_pinned(payload, (size_t)np * kPayloadStride) &&
-                       zrx_io::is_pinned(pkt_info, (size_t)np * 32);
-  if ((!pin_in && io->reserve_in(in_max) != hipSuccess) || (!pin_out && io->reserve_out(out_max) != hipSuccess) ||
+  const uint8_t* hs = a.sym + (size_t)base * 256;
+  const uint8_t* hchan = a.chan ? a.chan + (size_t)q0 * 256 : nullptr;
+  unsigned char* payload = a.payload + (size_t)q0 * kPayloadStride;
+  int32_t* pkt_info = a.info + 8 * (size_t)q0;
+  if ((!a.pin_in && io->reserve_in(in_max) != hipSuccess) || (!a.pin_out && io->reserve_out(out_max) != hipSuccess) ||
       io->reserve_flags(nch) != hipSuccess)
     return ZRX_ENOMEM;
   auto run = [&]() -> int {
@@ -1177,76 +1316,114 @@ int32_t wifi_rx_batch(struct complex16* sym, int nsym_total, const int32_t* pkt_
     };
     for (int j = 0; j < nch; j++) {
       const int slot = j & 1, p0 = cut[j], p1 = cut[j + 1], n = p1 - p0;
-      const size_t s0 = (size_t)pkt_sym_off[p0] * 256, sb = (size_t)(pkt_sym_off[p1] - pkt_sym_off[p0]) * 256;
+      const size_t s0 = (size_t)off[p0] * 256, sb = (size_t)((p1 < np ? off[p1] : nsym) - off[p0]) * 256;
       const uint8_t* src = hs + s0;
-      const uint8_t* csrc = chan ? (const uint8_t*)chan + (size_t)p0 * 256 : nullptr;
-      if (!pin_in) {
+      const uint8_t* csrc = hchan ? hchan + (size_t)p0 * 256 : nullptr;
+      if (!a.pin_in) {
         ZRX_CHECK(hipEventSynchronize(io->up_done[slot]));   // the slot's last upload is done
         zrx_io::par_copy(*io->pool, io->in[slot], src, sb);
-        if (chan) std::memcpy(io->in[slot] + sb, csrc, (size_t)n * 256);
+        if (csrc) std::memcpy(io->in[slot] + sb, csrc, (size_t)n * 256);
         src = io->in[slot];
-        csrc = io->in[slot] + sb;
+        csrc = csrc ? io->in[slot] + sb : nullptr;
       }
       if (sb) ZRX_CHECK(hipMemcpyAsync(d_sym + s0, src, sb, hipMemcpyHostToDevice, io->up));
-      if (chan) ZRX_CHECK(hipMemcpyAsync(d_chan + (size_t)p0 * 256, csrc, (size_t)n * 256, hipMemcpyHostToDevice, io->up));
+      if (csrc) ZRX_CHECK(hipMemcpyAsync(d_chan + (size_t)p0 * 256, csrc, (size_t)n * 256, hipMemcpyHostToDevice, io->up));
       ZRX_CHECK(hipEventRecord(io->up_done[slot], io->up));
       ZRX_CHECK(hipStreamWaitEvent(c->stream, io->up_done[slot], 0));
       uint8_t* dp = d_pay + (size_t)p0 * kPayloadStride;
       if (cw[j]) ZRX_CHECK(hipMemset2DAsync(dp, kPayloadStride, 0, cw[j], n, c->stream));
       const int r = rx_chain(c, (const complex16*)d_sym, d_off + p0, d_ns + p0, n, cmax[j],
-                             chan ? (const complex16*)(d_chan + (size_t)p0 * 256) : nullptr, dp, d_info + 8 * (size_t)p0);
+                             hchan ? (const complex16*)(d_chan + (size_t)p0 * 256) : nullptr, dp,
+                             d_info + 8 * (size_t)p0);
       if (r) return r;
       ZRX_CHECK(hipMemcpyAsync(io->flags + j, c->nrows + v3::kPlanDropped, 4, hipMemcpyDeviceToHost, c->stream));
       ZRX_CHECK(hipEventRecord(io->decoded, c->stream));
       ZRX_CHECK(hipStreamWaitEvent(io->down, io->decoded, 0));
-      uint8_t* oi = pin_out ? (uint8_t*)(pkt_info + 8 * (size_t)p0) : io->out[slot];
-      uint8_t* op = pin_out ? payload + (size_t)p0 * kPayloadStride : io->out[slot] + (size_t)n * 32;
+      uint8_t* oi = a.pin_out ? (uint8_t*)(pkt_info + 8 * (size_t)p0) : io->out[slot];
+      uint8_t* op = a.pin_out ? payload + (size_t)p0 * kPayloadStride : io->out[slot] + (size_t)n * 32;
       ZRX_CHECK(hipMemcpyAsync(oi, d_info + 8 * (size_t)p0, (size_t)n * 32, hipMemcpyDeviceToHost, io->down));
       if (cw[j])
-        ZRX_CHECK(hipMemcpy2DAsync(op, pin_out ? (size_t)kPayloadStride : (size_t)cw[j], dp, kPayloadStride, cw[j], n,
-                                   hipMemcpyDeviceToHost, io->down));
+        ZRX_CHECK(hipMemcpy2DAsync(op, a.pin_out ? (size_t)kPayloadStride : (size_t)cw[j], dp, kPayloadStride, cw[j],
+                                   n, hipMemcpyDeviceToHost, io->down));
       ZRX_CHECK(hipEventRecord(io->down_done[slot], io->down));
-      if (!pin_out && j >= 1) {
+      if (!a.pin_out && j >= 1) {
         const int r2 = drain(j - 1);                   // (overlaps chunk j's transfers and decode)
         if (r2) return r2;
       }
     }
-    return pin_out ? ZRX_OK : drain(nch - 1);
+    return a.pin_out ? ZRX_OK : drain(nch - 1);
   };
   rc = run();
   host_io_quiesce(c);
   if (rc) return rc;
   rc = plan_flags_ok(io, nch);
   if (rc) return rc;
+  // every CRC-passing payload fits the bytes its chunk brought back (cw): a kernel writing
+  // more than 216 bits a data symbol would otherwise hand back a cut payload marked good
   int ok = 0;
-  for (int i = 0; i < np; i++) ok += pkt_info[8 * i + 4] != 0;
+  for (int j = 0; j < nch; j++)
+    for (int i = cut[j]; i < cut[j + 1]; i++) {
+      const int32_t* inf = pkt_info + 8 * (size_t)i;
+      if (inf[4] == 0) continue;
+      if (inf[2] - 4 > cw[j]) {
+        std::fprintf(stderr, "ziria_rx: packet %d carries %d payload bytes, past the %d its chunk returned\n", q0 + i,
+                     inf[2] - 4, cw[j]);
+        return ZRX_EINTERNAL;
+      }
+      ok++;
+    }
   return ok;
 }
 
-
-int32_t wifi_rx_stream_batch(struct complex16* samples, int nsamples, const int32_t* cap_off, int n_off,
-                             int downsample, unsigned char* payload, int payload_len_bits,
-                             int32_t* pkt_info, int n_info, int32_t* det, int n_det) {
-  const int nc = n_off - 1;
-  if (nc < 0 || nsamples < 0 || n_info < 8 * nc || n_det < fe::kDetWords * nc ||
-      (int64_t)payload_len_bits / 8 < (int64_t)nc * kPayloadStride)
+int32_t wifi_rx_batch(struct complex16* sym, int nsym_total, const int32_t* pkt_sym_off, int n_off,
+                      const struct complex16* chan, int chan_len, unsigned char* payload, int payload_len_bits,
+                      int32_t* pkt_info, int n_info) {
+  const int np = n_off - 1;
+  if (np < 0 || nsym_total < 0 || n_info < 8 * np || (int64_t)payload_len_bits / 8 < (int64_t)np * kPayloadStride)
     return ZRX_EINVAL;
-  if (nc == 0) return 0;
+  if (chan && chan_len < 64 * (int64_t)np) return ZRX_EINVAL;
+  if (np == 0) return 0;
+  for (int i = 0; i < np; i++)
+    if (pkt_sym_off[i] < 0 || pkt_sym_off[i + 1] < pkt_sym_off[i] || pkt_sym_off[i + 1] > nsym_total) return ZRX_EINVAL;
+  std::lock_guard<std::mutex> lk(g_mu);
+  const int rc0 = node_resolve();
+  if (rc0) return rc0;
+  const uint8_t* hs = (const uint8_t*)sym;
+  RxCall a{hs, pkt_sym_off, (const uint8_t*)chan, payload, pkt_info, false, false};
+  a.pin_in = registered(hs + (size_t)pkt_sym_off[0] * 256, (size_t)(pkt_sym_off[np] - pkt_sym_off[0]) * 256) &&
+             (!chan || registered(chan, (size_t)np * 256));
+  a.pin_out = registered(payload, (size_t)np * kPayloadStride) && registered(pkt_info, (size_t)np * 32);
+  const size_t cb = chan ? 256 : 0;
+  return node_run(np, [&](int i) { return (int64_t)pkt_sym_off[i] * 256 + (int64_t)cb * i; },
+                  [&](zrx_ctx* c, int q0, int q1) { return rx_range(c, a, q0, q1); });
+}
+
+// ---- receiver() batch over captures [q0, q1) of one shard: the device holds only its samples
+struct StreamCall {
+  const uint8_t* samples;                  // 4 B per sample
+  const int32_t* cap_off;                  // n + 1 (validated)
+  int downsample;
+  unsigned char* payload;
+  int32_t* info;
+  int32_t* det;
+};
+
+static int stream_range(zrx_ctx* c, const StreamCall& a, int q0, int q1) {
+  const int nc = q1 - q0;
+  if (nc <= 0) return 0;
+  const int64_t base = a.cap_off[q0], nsamp = a.cap_off[q1] - base;
   std::vector<int64_t> off(nc);
   std::vector<int32_t> len(nc);
   int max_len = 0;
   for (int i = 0; i < nc; i++) {
-    if (cap_off[i] < 0 || cap_off[i + 1] < cap_off[i] || cap_off[i + 1] > nsamples) return ZRX_EINVAL;
-    off[i] = cap_off[i];
-    len[i] = cap_off[i + 1] - cap_off[i];
+    off[i] = a.cap_off[q0 + i] - base;
+    len[i] = a.cap_off[q0 + i + 1] - a.cap_off[q0 + i];
     max_len = std::max(max_len, len[i]);
   }
-  std::lock_guard<std::mutex> lk(g_mu);
-  zrx_ctx* c = default_ctx();
-  if (!c) return ZRX_ENODEV;
-  const size_t s_smp = ((size_t)nsamples * 4 + 255) / 256 * 256 + 256;
-  const size_t s_off = ((size_t)nc * 8 + 255) / 256 * 256, s_len = ((size_t)nc * 4 + 255) / 256 * 256;
-  const size_t s_pay = (size_t)nc * kPayloadStride, s_info = ((size_t)nc * 32 + 255) / 256 * 256;
+  const auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+  const size_t s_smp = al((size_t)nsamp * 4) + 256;
+  const size_t s_off = al((size_t)nc * 8), s_len = al((size_t)nc * 4);
+  const size_t s_pay = (size_t)nc * kPayloadStride, s_info = al((size_t)nc * 32);
   const size_t s_det = (size_t)nc * 4 * fe::kDetWords;
   uint8_t* d = (uint8_t*)staging(c, s_smp + s_off + s_len + s_pay + s_info + s_det + 1024);
   if (!d) return ZRX_ENOMEM;
@@ -1256,65 +1433,111 @@ int32_t wifi_rx_stream_batch(struct complex16* samples, int nsamples, const int3
   uint8_t* d_pay = (uint8_t*)d_len + s_len;
   int32_t* d_info = (int32_t*)(d_pay + s_pay);
   int32_t* d_det = (int32_t*)((uint8_t*)d_info + s_info);
-  ZRX_CHECK(hipMemcpyAsync(d_smp, samples, (size_t)nsamples * 4, hipMemcpyHostToDevice, c->stream));
-  ZRX_CHECK(hipMemcpyAsync(d_off, off.data(), (size_t)nc * 8, hipMemcpyHostToDevice, c->stream));
-  ZRX_CHECK(hipMemcpyAsync(d_len, len.data(), (size_t)nc * 4, hipMemcpyHostToDevice, c->stream));
-  ZRX_CHECK(hipMemsetAsync(d_pay, 0, s_pay, c->stream));
-  int rc = zrx_rx_stream_dev(c, (const complex16*)d_smp, d_off, d_len, nc, max_len, downsample, d_pay, d_info, d_det);
+  unsigned char* payload = a.payload + (size_t)q0 * kPayloadStride;
+  int32_t* info = a.info + 8 * (size_t)q0;
+  int32_t* det = a.det + (size_t)fe::kDetWords * q0;
+  auto run = [&]() -> int {
+    ZRX_CHECK(hipMemcpyAsync(d_smp, a.samples + (size_t)base * 4, (size_t)nsamp * 4, hipMemcpyHostToDevice, c->stream));
+    ZRX_CHECK(hipMemcpyAsync(d_off, off.data(), (size_t)nc * 8, hipMemcpyHostToDevice, c->stream));
+    ZRX_CHECK(hipMemcpyAsync(d_len, len.data(), (size_t)nc * 4, hipMemcpyHostToDevice, c->stream));
+    ZRX_CHECK(hipMemsetAsync(d_pay, 0, s_pay, c->stream));
+    const int r = zrx_rx_stream_dev(c, (const complex16*)d_smp, d_off, d_len, nc, max_len, a.downsample, d_pay,
+                                    d_info, d_det);
+    if (r) return r;
+    ZRX_CHECK(hipMemcpyAsync(payload, d_pay, s_pay, hipMemcpyDeviceToHost, c->stream));
+    ZRX_CHECK(hipMemcpyAsync(info, d_info, (size_t)nc * 32, hipMemcpyDeviceToHost, c->stream));
+    ZRX_CHECK(hipMemcpyAsync(det, d_det, s_det, hipMemcpyDeviceToHost, c->stream));
+    return ZRX_OK;
+  };
+  int rc = run();
+  (void)hipStreamSynchronize(c->stream);             // (nothing in flight on any return)
   if (rc) return rc;
-  ZRX_CHECK(hipMemcpyAsync(payload, d_pay, s_pay, hipMemcpyDeviceToHost, c->stream));
-  ZRX_CHECK(hipMemcpyAsync(pkt_info, d_info, (size_t)nc * 32, hipMemcpyDeviceToHost, c->stream));
-  ZRX_CHECK(hipMemcpyAsync(det, d_det, s_det, hipMemcpyDeviceToHost, c->stream));
-  ZRX_CHECK(hipStreamSynchronize(c->stream));
   rc = zrx_plan_check(c);                            // rows dropped by the plan: ZRX_EPLAN, never silent
   if (rc) return rc;
   int ok = 0;
-  for (int i = 0; i < nc; i++) ok += det[fe::kDetWords * i] && pkt_info[8 * i + 4] != 0;
+  for (int i = 0; i < nc; i++) ok += det[fe::kDetWords * i] && info[8 * i + 4] != 0;
   return ok;
 }
 
+int32_t wifi_rx_stream_batch(struct complex16* samples, int nsamples, const int32_t* cap_off, int n_off,
+                             int downsample, unsigned char* payload, int payload_len_bits,
+                             int32_t* pkt_info, int n_info, int32_t* det, int n_det) {
+  const int nc = n_off - 1;
+  if (nc < 0 || nsamples < 0 || n_info < 8 * nc || n_det < fe::kDetWords * nc ||
+      (int64_t)payload_len_bits / 8 < (int64_t)nc * kPayloadStride)
+    return ZRX_EINVAL;
+  if (nc == 0) return 0;
+  for (int i = 0; i < nc; i++)
+    if (cap_off[i] < 0 || cap_off[i + 1] < cap_off[i] || cap_off[i + 1] > nsamples) return ZRX_EINVAL;
+  std::lock_guard<std::mutex> lk(g_mu);
+  const StreamCall a{(const uint8_t*)samples, cap_off, downsample, payload, pkt_info, det};
+  return node_run(nc, [&](int i) { return (int64_t)cap_off[i] * 4; },
+                  [&](zrx_ctx* c, int q0, int q1) { return stream_range(c, a, q0, q1); });
+}
+
+// ---- transmitter() batch over packets [q0, q1) of one shard
+struct TxCall {
+  const unsigned char* in;
+  const int32_t* in_off;                   // n + 1 (validated)
+  struct complex16* out;
+  const int32_t* out_off;                  // n + 1 (filled by the call)
+};
+
+static int tx_range(zrx_ctx* c, const TxCall& a, int q0, int q1) {
+  const int np = q1 - q0;
+  if (np <= 0) return 0;
+  const int64_t ib = a.in_off[q0], ob = a.out_off[q0];
+  const int64_t in_bytes = a.in_off[q1] - ib, nsamp = a.out_off[q1] - ob;
+  std::vector<int64_t> ioff(np), ooff(np);
+  for (int i = 0; i < np; i++) {
+    ioff[i] = a.in_off[q0 + i] - ib;
+    ooff[i] = a.out_off[q0 + i] - ob;
+  }
+  const auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+  const size_t s_in = al((size_t)in_bytes) + 256, s_off = al((size_t)np * 8);
+  const size_t s_out = (size_t)nsamp * 4;
+  uint8_t* d = (uint8_t*)staging(c, s_in + 2 * s_off + al((size_t)np * 4) + s_out + 1024);
+  if (!d) return ZRX_ENOMEM;
+  uint8_t* d_in = d;
+  int64_t* d_ioff = (int64_t*)(d + s_in);
+  int64_t* d_ooff = (int64_t*)((uint8_t*)d_ioff + s_off);
+  int32_t* d_ns = (int32_t*)((uint8_t*)d_ooff + s_off);
+  uint8_t* d_out = (uint8_t*)d_ns + al((size_t)np * 4);
+  auto run = [&]() -> int {
+    ZRX_CHECK(hipMemcpyAsync(d_in, a.in + ib, (size_t)in_bytes, hipMemcpyHostToDevice, c->stream));
+    ZRX_CHECK(hipMemcpyAsync(d_ioff, ioff.data(), (size_t)np * 8, hipMemcpyHostToDevice, c->stream));
+    ZRX_CHECK(hipMemcpyAsync(d_ooff, ooff.data(), (size_t)np * 8, hipMemcpyHostToDevice, c->stream));
+    const int r = zrx_tx_dev(c, d_in, d_ioff, np, (complex16*)d_out, d_ooff, d_ns);
+    if (r) return r;
+    ZRX_CHECK(hipMemcpyAsync((uint8_t*)a.out + (size_t)ob * 4, d_out, s_out, hipMemcpyDeviceToHost, c->stream));
+    return ZRX_OK;
+  };
+  const int rc = run();
+  (void)hipStreamSynchronize(c->stream);             // (nothing in flight on any return)
+  return rc ? rc : (int)nsamp;
+}
 
 int32_t wifi_tx_batch(const unsigned char* in, int inlen, const int32_t* pkt_in_off, int n_off,
                       struct complex16* out, int outlen, int32_t* pkt_out_off, int n_oo) {
   const int np = n_off - 1;
   if (np < 0 || inlen < 0 || n_oo < np + 1) return ZRX_EINVAL;
   if (np == 0) { pkt_out_off[0] = 0; return 0; }
-  std::vector<int64_t> ioff(np), ooff(np);
   int64_t total = 0;
   for (int i = 0; i < np; i++) {
     if (pkt_in_off[i] < 0 || pkt_in_off[i + 1] - pkt_in_off[i] < 3 || pkt_in_off[i + 1] > inlen) return ZRX_EINVAL;
     const uint8_t* h = in + pkt_in_off[i];
     const int len = std::min((int)((((uint32_t)h[1] << 8 | h[0]) >> 5 | (uint32_t)h[2] << 11) & 0xFFF), 2048);
     if (pkt_in_off[i] + 3 + std::max(len - 4, 0) > pkt_in_off[i + 1]) return ZRX_EINVAL;   // payload bytes present
-    ioff[i] = pkt_in_off[i];
-    ooff[i] = total;
     pkt_out_off[i] = (int32_t)total;
     total += zrx_tx_samples(h);
+    if (total > outlen) return ZRX_EINVAL;
   }
   pkt_out_off[np] = (int32_t)total;
-  if (total > outlen) return ZRX_EINVAL;
   std::lock_guard<std::mutex> lk(g_mu);
-  zrx_ctx* c = default_ctx();
-  if (!c) return ZRX_ENODEV;
-  const size_t s_in = ((size_t)inlen + 255) / 256 * 256 + 256, s_off = ((size_t)np * 8 + 255) / 256 * 256;
-  const size_t s_out = (size_t)total * 4;
-  uint8_t* d = (uint8_t*)staging(c, s_in + 2 * s_off + s_off / 2 + s_out + 1024);
-  if (!d) return ZRX_ENOMEM;
-  uint8_t* d_in = d;
-  int64_t* d_ioff = (int64_t*)(d + s_in);
-  int64_t* d_ooff = (int64_t*)((uint8_t*)d_ioff + s_off);
-  int32_t* d_ns = (int32_t*)((uint8_t*)d_ooff + s_off);
-  uint8_t* d_out = (uint8_t*)d_ns + (s_off / 2 + 255) / 256 * 256;
-  ZRX_CHECK(hipMemcpyAsync(d_in, in, (size_t)inlen, hipMemcpyHostToDevice, c->stream));
-  ZRX_CHECK(hipMemcpyAsync(d_ioff, ioff.data(), (size_t)np * 8, hipMemcpyHostToDevice, c->stream));
-  ZRX_CHECK(hipMemcpyAsync(d_ooff, ooff.data(), (size_t)np * 8, hipMemcpyHostToDevice, c->stream));
-  int rc = zrx_tx_dev(c, d_in, d_ioff, np, (complex16*)d_out, d_ooff, d_ns);
-  if (rc) return rc;
-  ZRX_CHECK(hipMemcpyAsync(out, d_out, s_out, hipMemcpyDeviceToHost, c->stream));
-  ZRX_CHECK(hipStreamSynchronize(c->stream));
-  return (int32_t)total;
+  const TxCall a{in, pkt_in_off, out, pkt_out_off};
+  return node_run(np, [&](int i) { return (int64_t)pkt_out_off[i] * 4; },
+                  [&](zrx_ctx* c, int q0, int q1) { return tx_range(c, a, q0, q1); });
 }
-
 
 }  // namespace zrx_batch
 
@@ -1351,6 +1574,64 @@ int32_t __ext_wifi_rx_stream_batch(struct complex16* samples, int nsamples, int3
 int32_t __ext_wifi_tx_batch(unsigned char* in, int inlen, int32_t* pkt_in_off, int n_off,
                             struct complex16* out, int outlen, int32_t* pkt_out_off, int n_oo) {
   return zrx_batch::wifi_tx_batch(in, inlen, pkt_in_off, n_off, out, outlen, pkt_out_off, n_oo);
+}
+
+// ---- the node behind the batched externals
+int zrx_set_devices(const int32_t* devices, int n, int64_t min_shard_bytes) {
+  if (n < 0 || (n > 0 && !devices)) return ZRX_EINVAL;
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (int i = 0; i < n; i++)
+    if (check_device(devices[i]) != ZRX_OK) return ZRX_ENODEV;
+  node_reset();
+  g_node.want.assign(devices, devices + n);
+  g_node.min_shard_bytes = min_shard_bytes < 0 ? zrx_shard::kMinShardBytes : min_shard_bytes;
+  return ZRX_OK;
+}
+
+int zrx_get_devices(int32_t* devices, int cap) {
+  if (cap < 0 || (cap > 0 && !devices)) return ZRX_EINVAL;
+  std::lock_guard<std::mutex> lk(g_mu);
+  const int rc = node_resolve();
+  if (rc) return rc;
+  for (int i = 0; i < std::min(cap, (int)g_node.dev.size()); i++) devices[i] = g_node.dev[(size_t)i];
+  return (int)g_node.dev.size();
+}
+
+int zrx_node_stats(int64_t* stats8) {
+  if (!stats8) return ZRX_EINVAL;
+  std::lock_guard<std::mutex> lk(g_mu);
+  stats8[0] = g_node.last_shards;
+  g_node.reg.stats(stats8 + 1);
+  stats8[7] = (int64_t)g_node.min_shard_bytes;
+  return ZRX_OK;
+}
+
+int zrx_set_host_register(int mode) {
+  if (mode < 0 || mode > 2) return ZRX_EINVAL;
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_node.reg.set_mode(mode);
+  return ZRX_OK;
+}
+
+int zrx_shard_split(const int64_t* prefix, int np, int nshards, int64_t min_bytes, int32_t* cut) {
+  if (np < 0 || nshards < 1 || !cut || (np > 0 && !prefix)) return ZRX_EINVAL;
+  for (int i = 0; i < np; i++)
+    if (prefix[i + 1] < prefix[i]) return ZRX_EINVAL;
+  const std::vector<int> c = zrx_shard::split(np, [&](int i) { return prefix[i]; }, nshards, min_bytes);
+  for (size_t k = 0; k < c.size(); k++) cut[k] = c[k];
+  return (int)c.size() - 1;
+}
+
+int zrx_shard_selftest(const int64_t* prefix, int np, int nshards, int64_t min_bytes, int32_t* owner,
+                       int fail_shard) {
+  if (np < 0 || nshards < 1 || !owner || (np > 0 && !prefix)) return ZRX_EINVAL;
+  const std::vector<int> cut = zrx_shard::split(np, [&](int i) { return prefix[i]; }, nshards, min_bytes);
+  zrx_io::Pool pool(nshards);
+  return zrx_shard::run(&pool, cut, [&](int k, int p0, int p1) -> int {
+    if (k == fail_shard) return ZRX_EINTERNAL;
+    for (int i = p0; i < p1; i++) owner[i] = k;
+    return p1 - p0;
+  });
 }
 
 }  // extern "C"

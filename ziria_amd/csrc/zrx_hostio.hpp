@@ -163,7 +163,9 @@ struct HostIO {
   Pool* pool = nullptr;
 
   ~HostIO() {
-    (void)hipSetDevice(device);
+    int prev = -1;
+    if (hipGetDevice(&prev) == hipSuccess && prev != device) (void)hipSetDevice(device);
+    else prev = -1;
     for (int s = 0; s < 2; s++) {
       if (in[s]) (void)hipHostFree(in[s]);
       if (out[s]) (void)hipHostFree(out[s]);
@@ -175,23 +177,18 @@ struct HostIO {
     if (up) (void)hipStreamDestroy(up);
     if (down) (void)hipStreamDestroy(down);
     delete pool;
+    if (prev >= 0) (void)hipSetDevice(prev);          // (the caller's device, as it was)
   }
 
-  hipError_t init(int dev) {
+  // on device `dev` (the caller's current device is left as it was), with a host pool of
+  // `nthreads` threads for the pageable copies
+  hipError_t init(int dev, int nthreads) {
     device = dev;
-    hipError_t e;
-    if ((e = hipSetDevice(dev)) != hipSuccess) return e;
-    if ((e = hipStreamCreateWithFlags(&up, hipStreamNonBlocking)) != hipSuccess) return e;
-    if ((e = hipStreamCreateWithFlags(&down, hipStreamNonBlocking)) != hipSuccess) return e;
-    for (int s = 0; s < 2; s++) {
-      if ((e = hipEventCreateWithFlags(&up_done[s], hipEventDisableTiming)) != hipSuccess) return e;
-      if ((e = hipEventCreateWithFlags(&down_done[s], hipEventDisableTiming)) != hipSuccess) return e;
-    }
-    if ((e = hipEventCreateWithFlags(&decoded, hipEventDisableTiming | hipEventDisableSystemFence)) != hipSuccess)
-      return e;
-    const unsigned hc = std::thread::hardware_concurrency();
-    pool = new Pool((int)std::min(8u, std::max(1u, hc / 2)));
-    return hipSuccess;
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    const hipError_t e = init_on(dev, nthreads);
+    if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
+    return e;
   }
 
   // pinned slots of at least `bytes` each (grown on demand; every slot idle when called)
@@ -208,6 +205,20 @@ struct HostIO {
   }
 
  private:
+  hipError_t init_on(int dev, int nthreads) {
+    hipError_t e;
+    if ((e = hipSetDevice(dev)) != hipSuccess) return e;
+    if ((e = hipStreamCreateWithFlags(&up, hipStreamNonBlocking)) != hipSuccess) return e;
+    if ((e = hipStreamCreateWithFlags(&down, hipStreamNonBlocking)) != hipSuccess) return e;
+    for (int s = 0; s < 2; s++) {
+      if ((e = hipEventCreateWithFlags(&up_done[s], hipEventDisableTiming)) != hipSuccess) return e;
+      if ((e = hipEventCreateWithFlags(&down_done[s], hipEventDisableTiming)) != hipSuccess) return e;
+    }
+    if ((e = hipEventCreateWithFlags(&decoded, hipEventDisableTiming | hipEventDisableSystemFence)) != hipSuccess)
+      return e;
+    pool = new Pool(std::max(1, nthreads));
+    return hipSuccess;
+  }
   static hipError_t grow(uint8_t* (&slot)[2], size_t& cap, size_t bytes) {
     if (bytes <= cap) return hipSuccess;
     const size_t c = std::max(bytes, size_t(1) << 20);

@@ -176,3 +176,40 @@ def wifi_tx_batch(packets):
     if rc < 0:
         raise ZiriaRxError(f"__ext_wifi_tx_batch failed ({rc})")
     return out[:total], ooff
+
+
+# ------------------------------------------------------------------ the node behind Part 2
+def set_devices(devices=None, min_shard_bytes=-1):
+    """Logical shards of the batched externals (zrx_set_devices): a list of device ids (a
+    device may repeat), or None for the default (ZRX_DEVICES, else every gfx950 device);
+    min_shard_bytes < 0 keeps the default 16 MiB, 0 spreads every call over every shard."""
+    d = np.ascontiguousarray(devices if devices is not None else [], np.int32)
+    rc = lib().zrx_set_devices(_p(d) if d.size else None, int(d.size), int(min_shard_bytes))
+    if rc < 0:
+        raise ZiriaRxError(f"zrx_set_devices failed ({rc})")
+
+
+def get_devices():
+    d = np.zeros(64, np.int32)
+    n = lib().zrx_get_devices(_p(d), d.size)
+    if n < 0:
+        raise ZiriaRxError(f"zrx_get_devices failed ({n})")
+    return [int(x) for x in d[:n]]
+
+
+NODE_STATS = ("last_shards", "register_mode", "registered_ranges", "registered_bytes", "registrations",
+              "register_hits", "register_failures", "min_shard_bytes")
+
+
+def node_stats():
+    s = np.zeros(8, np.int64)
+    lib().zrx_node_stats(_p(s))
+    return dict(zip(NODE_STATS, (int(x) for x in s)))
+
+
+def set_host_register(mode):
+    """0 = never page-lock caller arrays, 1 = the main program's static arrays (default), 2 =
+    also other arrays >= 256 KiB (the caller keeps them mapped until mode 0 or 1)."""
+    rc = lib().zrx_set_host_register(int(mode))
+    if rc < 0:
+        raise ZiriaRxError(f"zrx_set_host_register failed ({rc})")

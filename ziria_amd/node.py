@@ -104,6 +104,17 @@ def max_over_ranks(seconds, device=None):
     return float(t.item())
 
 
+def all_gather_floats(values, device=None):
+    """Every rank's list of floats (same length on every rank), in rank order."""
+    world, _ = world_rank()
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=comm_device(device))
+    if world == 1:
+        return [t.tolist()]
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [o.tolist() for o in out]
+
+
 def barrier(device=None):
     if world_rank()[0] > 1:
         dist.barrier()
@@ -115,7 +126,7 @@ def _sync(device):
 
 
 def run_sharded(total, make_shard, step, outputs, expected, steps, warmup, payload_len, device=None,
-                crc_ok_only=False, on_timed=None, nbatches=1):
+                crc_ok_only=False, on_timed=None, nbatches=1, on_step=None):
     """The bench's N-rank loop over one global batch of `total` packets.
 
     make_shard(lo, hi) builds this rank's packets [lo, hi) (already in device memory) as
@@ -128,6 +139,8 @@ def run_sharded(total, make_shard, step, outputs, expected, steps, warmup, paylo
     every gathered packet of every batch.
     on_timed(True) is called after the warmup, before the barrier that opens the timed region
     (bench.py runs its instrumented stage-timer pass there), on_timed(False) after it closes.
+    on_step(i), when given, is called at the start of the timed region (i = -1) and after each
+    timed step i (bench.py records a HIP event there: per-step times).
 
     Timing: `warmup` untimed steps, then barrier + device sync, `steps` timed steps, device
     sync + barrier, and the slowest rank's time.  Returns on every rank a dict with the
@@ -148,17 +161,23 @@ def run_sharded(total, make_shard, step, outputs, expected, steps, warmup, paylo
     barrier(device)
     _sync(device)
     t0 = time.perf_counter()
+    if on_step:
+        on_step(-1)
     timed_batches = []
-    for _ in range(steps):
+    for i in range(steps):
         step(shard, k)
+        if on_step:
+            on_step(i)
         timed_batches.append(k % nbatches)
         k += 1
     _sync(device)
+    t_own = time.perf_counter() - t0                 # this rank's own time (before the closing barrier)
     barrier(device)
     t1 = time.perf_counter()
     if on_timed:
         on_timed(False)
     elapsed = max_over_ranks(t1 - t0, device=device)
+    rank_elapsed = [r[0] for r in all_gather_floats([t_own], device=device)]
 
     L = payload_len
     ok_b, bits_b, pay_b, info_b = [], [], [], []
@@ -184,7 +203,8 @@ def run_sharded(total, make_shard, step, outputs, expected, steps, warmup, paylo
         pay_b.append(pay_all)
         info_b.append(info_all)
     bits_per_step = sum(bits_b[b] for b in timed_batches) / max(steps, 1)
-    res = dict(lo=lo, hi=hi, shard=shard, elapsed=elapsed, steps=steps, ok=sum(ok_b), bits=bits_per_step,
+    res = dict(lo=lo, hi=hi, shard=shard, elapsed=elapsed, rank_elapsed=rank_elapsed, steps=steps, ok=sum(ok_b),
+               bits=bits_per_step,
                bits_per_batch=bits_b, gather_s=gather_s / max(nbatches, 1), world=world, rank=rank, batches=nbatches)
     if rank == 0:
         packets = mism = 0
