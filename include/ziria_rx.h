@@ -288,7 +288,7 @@ int zrx_node_stats(int64_t* stats8);
 /* Page-locking of the caller's host arrays, so their copies skip the pinned staging slots:
  * 0 = never; 1 (default, or ZRX_HOST_REGISTER=1) = arrays in the main program's static
  * storage (.data/.bss: where wplc puts a program's arrays; never unmapped), registered on first
- * use and kept; 2 = also any other array of at least 256 KiB, on first use -- the caller keeps
+ * use and kept; 2 = also any other array of at least 32 KiB, on first use -- the caller keeps
  * those arrays mapped until it sets mode 0 or 1, which releases them (a page-lock must not
  * outlive its memory).  Memory the caller pinned itself is always used in place. */
 int zrx_set_host_register(int mode);

@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 for r in $(seq ${ROUNDS:-2}); do
   for v in ${VARIANTS:-cur}; do
     if [ "$v" = cur ]; then unset ZRX_LIB_VARIANT; else export ZRX_LIB_VARIANT=$v; fi
-    timeout -k 10 200 python bench.py --steps ${STEPS:-5} --warmup 2 --no-cpu ${BENCH_ARGS:-} > gpurun_out/ab${AB_TAG:-}_${v}_$r.log 2>&1; rc=$?
+    timeout -k 10 200 python bench.py --steps ${STEPS:-5} --warmup 2 --no-cpu --no-sub ${BENCH_ARGS:-} > gpurun_out/ab${AB_TAG:-}_${v}_$r.log 2>&1; rc=$?
     [ $rc -eq 0 ] || { echo "$v rc=$rc"; tail -5 gpurun_out/ab${AB_TAG:-}_${v}_$r.log; exit $rc; }
     python -c "
 import json

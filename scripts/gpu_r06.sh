@@ -14,6 +14,18 @@ if [ -z "$SKIP_PYTEST" ]; then
   echo "pytest rc=$rc"; tail -3 gpurun_out/${T}_pytest_gpu.log
   [ $rc -eq 0 ] || exit $rc
 fi
+if [ -n "$AB" ]; then
+  step ab
+  VARIANTS="$AB" ROUNDS=${ROUNDS:-3} STEPS=${STEPS:-20} ./scripts/gpu_ab_lib.sh > gpurun_out/${T}_ab.txt 2>&1; rc=$?
+  cat gpurun_out/${T}_ab.txt
+  [ $rc -eq 0 ] || exit $rc
+fi
+if [ -n "$AB_EQ" ]; then
+  step ab-eq
+  VARIANTS="$AB_EQ" AB_TAG=eq ROUNDS=${ROUNDS:-3} STEPS=${STEPS:-20} BENCH_ARGS="--eq" ./scripts/gpu_ab_lib.sh > gpurun_out/${T}_ab_eq.txt 2>&1; rc=$?
+  cat gpurun_out/${T}_ab_eq.txt
+  [ $rc -eq 0 ] || exit $rc
+fi
 if [ -z "$SKIP_BENCH" ]; then
   step bench
   timeout -k 10 400 python -u bench.py ${BENCH_ARGS:---steps 20 --warmup 15} > gpurun_out/${T}_bench.log 2>&1; rc=$?

@@ -494,3 +494,27 @@ def test_chain_scrambler_states_and_short_payloads(engine, oracle):
         for i, r in enumerate(res):
             assert info[i, 2] == r["len"] == L + 4 and info[i, 4] == r["crc_ok"] == 1, (L, i)
             assert (pay[i, :L] == opay[i, :L]).all() and (pay[i, :L] == b["payload"][i]).all(), (L, i)
+
+
+@pytest.mark.parametrize("mixed", [False, True])
+def test_chain_plan_many_blocks(engine, mixed):
+    """k_pkt_scan over more than 64 blocks of 1024 packets (its look-back crosses several
+    64-record windows) and a partial last block: 66 x 1024 + 5 short packets, uniform (6 Mbps,
+    20-byte payloads) or mixed (8 MCS, PSDU 8..120 B); every packet's CRC passes with the
+    transmitted payload, so every offset, data-symbol prefix and wave start was right."""
+    n = 66 * 1024 + 5
+    if mixed:
+        m = txgen.make_mixed_fast(n, min_len=8, max_len=120, sigma=2.0, seed=0x66, device="cuda", chunk=8192)
+        lens = m["meta"][:, 2] - 4
+        pays = m["payload"]
+    else:
+        m = txgen.make_batch(n, mod=0, coding=0, payload_len=20, sigma=2.0, seed=0x66, device="cuda", chunk=8192)
+        lens = np.full(n, 20)
+        pays = m["payload"]
+    engine.reserve(n, m["max_nsym"])
+    pay, info = engine.rx(m["sym"], m["sym_off"], m["nsym"], m["max_nsym"])
+    pay, info = pay.cpu().numpy(), info.cpu().numpy()
+    assert (info[:, 4] == 1).all(), np.nonzero(info[:, 4] != 1)[0][:10]
+    for i in range(n):
+        assert (pay[i, :lens[i]] == np.asarray(pays[i])[:lens[i]]).all(), i
+    engine.plan_check()

@@ -69,6 +69,9 @@ struct zrx_ctx {
   uint8_t* segs = nullptr;        // segments per packet
   int32_t* order = nullptr;       // k_pkt_plan scratch: packets in row order
   uint2* dumps = nullptr;         // seam metric dumps, v3::seam_index
+  PlanScanRec* scan_rec = nullptr; // k_pkt_scan's per-block records (ceil(npkts / 4096) + 1)
+  uint32_t* scan_ctr = nullptr;   // its finished-block counter (reset by the last block)
+  uint32_t scan_epoch = 0;        // its ready mark, one per launch (never 0: records start zeroed)
   int64_t rows_cap = 0;
   bool use_order = true;          // ZRX_ORDER=0 (experiment builds) turns the plan off
   // The workspace is shared by every launch of this context: a launch on a different stream
@@ -126,8 +129,10 @@ static int check_device(int device) {
 static void free_ws(zrx_ctx* c) {
   for (void* p : {(void*)c->sig_soft, (void*)c->vparams, (void*)c->soft, (void*)c->soft_off, (void*)c->dsym,
                   (void*)c->wave_p0, (void*)c->dec, (void*)c->dec_off, (void*)c->dec_bits, (void*)c->rows,
-                  (void*)c->nrows, (void*)c->segs, (void*)c->dumps, (void*)c->order})
+                  (void*)c->nrows, (void*)c->segs, (void*)c->dumps, (void*)c->order, (void*)c->scan_rec,
+                  (void*)c->scan_ctr})
     (void)hipFree(p);
+  c->scan_rec = nullptr; c->scan_ctr = nullptr;
   c->sig_soft = nullptr; c->vparams = nullptr; c->soft = nullptr; c->soft_off = nullptr;
   c->dsym = nullptr; c->wave_p0 = nullptr; c->dec = nullptr; c->dec_off = nullptr; c->dec_bits = nullptr;
   c->rows = nullptr; c->nrows = nullptr; c->segs = nullptr; c->dumps = nullptr; c->order = nullptr; c->rows_cap = 0;
@@ -567,6 +572,11 @@ int zrx_reserve(zrx_ctx* c, int npkts, int max_nsym) {
   ZRX_CHECK(hipMalloc(&c->segs, (size_t)np + 16));
   ZRX_CHECK(hipMalloc(&c->order, (size_t)np * 4 + 16));
   ZRX_CHECK(hipMalloc(&c->dumps, (size_t)np * (v3::kMaxSeg - 1) * 2 * v3::kSeamWords * 8 + 256));
+  const size_t nrec = (size_t)np / kPsBlock + 2;
+  ZRX_CHECK(hipMalloc(&c->scan_rec, nrec * sizeof(PlanScanRec)));
+  ZRX_CHECK(hipMalloc(&c->scan_ctr, 64));
+  ZRX_CHECK(hipMemsetAsync(c->scan_rec, 0, nrec * sizeof(PlanScanRec), c->stream));
+  ZRX_CHECK(hipMemsetAsync(c->scan_ctr, 0, 64, c->stream));
   if (np > 0) {
     k_fill_offsets<<<blocks(np, 256), 256, 0, c->stream>>>(c->soft_off, np, stride);
     k_fill_offsets<<<blocks(np, 256), 256, 0, c->stream>>>(c->dec_off, np, kDecStride);
@@ -728,9 +738,12 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
                                         (int)plan_rows_max(c, npkts));
     ZRX_CHECK(hipEventRecord(c->ev_join, c->side));
   }
-  k_pkt_plan<<<1, 1024, 0, h>>>(c->vparams, npkts, c->soft_off, c->dsym, c->wave_p0, ordered ? c->rows : nullptr,
-                                c->nrows, c->segs, c->order, c->dec_bits, c->ncu, (int)plan_rows_max(c, npkts),
-                                split ? 1 : 0, ordered ? c->mixed_hint_dev : nullptr);
+  // the plan: offsets, the batch verdict and (unless split) a mixed batch's rows, over many blocks
+  if (++c->scan_epoch == 0) c->scan_epoch = 1;
+  k_pkt_scan<<<blocks(npkts, kPsBlock), kPsThreads, 0, h>>>(
+      c->vparams, npkts, c->soft_off, c->dsym, c->wave_p0, ordered ? c->rows : nullptr, ordered ? c->nrows : nullptr,
+      c->segs, c->order, c->dec_bits, c->ncu, (int)plan_rows_max(c, npkts), split ? 1 : 0,
+      ordered ? c->mixed_hint_dev : nullptr, c->scan_rec, c->scan_ctr, c->scan_epoch);
   if (ev) ZRX_CHECK(hipEventRecord(ev[2], h));
   // k_data_fft: waves over the batch's data symbols, at most npkts x (max_nsym - 1) of them
   const int fft_blocks = (int)std::min<int64_t>(((int64_t)npkts * (max_nsym - 1) + kDfThreads - 1) / kDfThreads,

@@ -544,6 +544,181 @@ __global__ __launch_bounds__(1024) void k_pkt_plan(const int32_t* __restrict__ v
   plan_rows_mixed(vparams, npkts, Lm, rows, nrows, segs, order, out_bits, ncu, rows_cap, hist, &rtotal);
 }
 
+// ---- k_pkt_scan: the rx chain's plan over many blocks ------------------------------------
+// k_pkt_plan's offsets scan (off, dsym, wave_p0) and its batch verdict (uniform or mixed:
+// the mixed-batch hint, the uniform plan header, a mixed batch's rows) in one launch of
+// ceil(npkts / 4096) blocks instead of one block's chain of dependent rounds (config 5: 28 us
+// on the head's critical path).  Each block takes 4096 consecutive packets (4 a thread),
+// publishes its sums (256-B soft units, data symbols, trellis columns, all-equal flag) in
+// rec[block] with the launch's epoch as the ready mark, adds the published sums of every block
+// before it (those were dispatched earlier and publish without waiting on anything, so the
+// spin always ends) and writes its packets' offsets.  The last block to finish (a counter it
+// resets) reduces the records and plans as k_pkt_plan did: the uniform header, or a mixed
+// batch's rows (plan_rows_mixed) unless k_pkt_rows does them beside k_data_fft (split).
+// nrows null: offsets only.
+constexpr int kPsThreads = 1024, kPsPer = 4, kPsBlock = kPsThreads * kPsPer;
+struct PlanScanRec {
+  uint32_t u, s;            // the block's 256-B soft units, data symbols
+  unsigned long long cols;  // its trellis columns
+  uint32_t same, ready;     // all its packets equal to packet 0; == epoch once published
+};
+__global__ __launch_bounds__(kPsThreads) void k_pkt_scan(const int32_t* __restrict__ vparams, int npkts,
+                                                         int64_t* __restrict__ off, int32_t* __restrict__ dsym,
+                                                         int32_t* __restrict__ wave_p0, int2* __restrict__ rows,
+                                                         int32_t* __restrict__ nrows, uint8_t* __restrict__ segs,
+                                                         int32_t* __restrict__ order, int32_t* __restrict__ out_bits,
+                                                         int ncu, int rows_cap, int split,
+                                                         int32_t* __restrict__ mixed_hint,
+                                                         PlanScanRec* __restrict__ rec, uint32_t* __restrict__ ctr,
+                                                         uint32_t epoch) {
+  constexpr int kW = kPsThreads / 64;
+  __shared__ uint32_t wsum_u[kW], wsum_s[kW], wflag[kW];
+  __shared__ unsigned long long wcols[kW];
+  __shared__ uint32_t pre_u, pre_s, last, rtotal;
+  __shared__ uint32_t hist[kOrderPerThread * 1024];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, b = blockIdx.x, nb = gridDim.x;
+  if (nrows) {
+    // (the reuse test of k_pkt_plan: every block reads the same words, and block 0 changes them
+    // only to values that make every later reader decide the same way)
+    const bool reuse = nrows[v3::kPlanExpN] == npkts && nrows[v3::kPlanMismatch] == 0;
+    if (reuse) {
+      if (b == 0 && t == 0) nrows[v3::kPlanFixes] = 0;
+      return;
+    }
+    if (b == 0 && t == 0) { nrows[v3::kPlanExpN] = 0; nrows[v3::kPlanMismatch] = 0; }
+  }
+  const int4 q0 = *reinterpret_cast<const int4*>(vparams);
+  const int p0 = b * kPsBlock + kPsPer * t;
+  uint32_t vu[kPsPer], vs[kPsPer], su = 0, ss = 0;
+  uint64_t my_cols = 0;
+  bool same = cols_of(q0.y, q0.z) > 0;
+#pragma unroll
+  for (int i = 0; i < kPsPer; i++) {
+    vu[i] = vs[i] = 0;
+    const int p = p0 + i;
+    if (p < npkts) {
+      const int4 q = *reinterpret_cast<const int4*>(vparams + 4 * (int64_t)p);   // {frame_len, cr, soft_len, mod}
+      const uint32_t n = (uint32_t)max(q.z, 0);
+      vu[i] = (n + 255u) >> 8;
+      vs[i] = q.w == 3 ? n / 288u : (n >> (q.w & 3)) / 48u;   // soft_len / N_CBPS
+      my_cols += cols_of(q.y, q.z);
+      same = same && q.x == q0.x && q.y == q0.y && q.z == q0.z && q.w == q0.w;
+    }
+    su += vu[i];
+    ss += vs[i];
+  }
+  // block scan of the threads' sums; the block's totals
+  const uint32_t iu = wave_incl_scan(su), is = wave_incl_scan(ss);
+  for (int o = 32; o > 0; o >>= 1) my_cols += (uint64_t)__shfl_xor((long long)my_cols, o);
+  const bool wsame = __builtin_amdgcn_ballot_w64(!same) == 0ull;
+  if (lane == 63) { wsum_u[wv] = iu; wsum_s[wv] = is; }
+  if (lane == 0) { wcols[wv] = my_cols; wflag[wv] = wsame ? 1u : 0u; }
+  __syncthreads();
+  uint32_t eu = iu - su, es = is - ss;
+  for (int w = 0; w < wv; w++) { eu += wsum_u[w]; es += wsum_s[w]; }
+  if (t == 0) {                                        // publish
+    uint32_t bu = 0, bs = 0, bf = 1;
+    unsigned long long bc = 0;
+    for (int w = 0; w < kW; w++) { bu += wsum_u[w]; bs += wsum_s[w]; bc += wcols[w]; bf &= wflag[w]; }
+    rec[b].u = bu;
+    rec[b].s = bs;
+    rec[b].cols = bc;
+    rec[b].same = bf;
+    __hip_atomic_store(&rec[b].ready, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (wv == 0) {                                       // every earlier block's sums
+    uint32_t au = 0, as = 0;
+    for (int j0 = 0; j0 < b; j0 += 64) {
+      const int j = j0 + lane;
+      if (j < b) {
+        while (__hip_atomic_load(&rec[j].ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != epoch)
+          __builtin_amdgcn_s_sleep(1);
+        au += rec[j].u;
+        as += rec[j].s;
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      au += (uint32_t)__shfl_xor((int)au, o);
+      as += (uint32_t)__shfl_xor((int)as, o);
+    }
+    if (lane == 0) { pre_u = au; pre_s = as; }
+  }
+  __syncthreads();
+  uint64_t u0 = (uint64_t)pre_u + eu;
+  uint32_t s0 = pre_s + es;
+#pragma unroll
+  for (int i = 0; i < kPsPer; i++) {
+    const int p = p0 + i;
+    if (p < npkts) {
+      off[p] = (int64_t)(u0 << 8);
+      dsym[p] = (int32_t)s0;
+      for (uint32_t w = (s0 + 63u) >> 6; 64u * w < s0 + vs[i]; w++) wave_p0[w] = p;
+    }
+    u0 += vu[i];
+    s0 += vs[i];
+  }
+  // the last block to get here reduces the records: the batch's totals and its verdict
+  __syncthreads();
+  if (t == 0) {
+    __threadfence();
+    last = atomicAdd(ctr, 1u) == (uint32_t)nb - 1u;
+    if (last) *ctr = 0u;                               // (ready for the next launch on this stream)
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  uint64_t tc = 0;
+  uint32_t ts = 0, all_same = 1;
+  for (int j = t; j < nb; j += kPsThreads) {
+    tc += rec[j].cols;
+    ts += rec[j].s;
+    all_same &= rec[j].same;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    tc += (uint64_t)__shfl_xor((long long)tc, o);
+    ts += (uint32_t)__shfl_xor((int)ts, o);
+  }
+  const bool ws = __builtin_amdgcn_ballot_w64(all_same == 0u) == 0ull;
+  __syncthreads();                                     // (the block's sums above were read)
+  if (lane == 0) { wcols[wv] = tc; wsum_s[wv] = ts; wflag[wv] = ws ? 1u : 0u; }
+  __syncthreads();
+  uint64_t tcols = 0;
+  uint32_t tsym = 0;
+  bool uniform = true;
+  for (int w = 0; w < kW; w++) { tcols += wcols[w]; tsym += wsum_s[w]; uniform = uniform && wflag[w]; }
+  if (t == 0) dsym[npkts] = (int32_t)tsym;             // the whole batch's data symbols
+  if (!nrows) return;
+  if (t == 0 && mixed_hint) *mixed_hint = uniform ? 0 : 1;   // (host-mapped: the next call's split choice)
+  const uint64_t rt = 64ull * (uint64_t)max(ncu, 1);   // rows that give every SIMD four waves
+  const uint32_t L0 = (uint32_t)min<uint64_t>((tcols + rt - 1) / rt, 0xFFFFFFFFull);
+  if (!uniform) {
+    if (split) {
+      if (t == 0) nrows[v3::kPlanUniform] = 0;         // (k_pkt_rows writes the same, beside k_data_fft)
+      return;
+    }
+    for (int i = t; i < kOrderPerThread * 1024; i += kPsThreads) hist[i] = 0;
+    if (t == 0) rtotal = 0;
+    __syncthreads();
+    const uint32_t L = max(L0, v3::kMinSeg);
+    const uint32_t Lm = max(L * v3::kSegMixNum / 8u, v3::kMinSeg);
+    plan_rows_mixed(vparams, npkts, Lm, rows, nrows, segs, order, out_bits, ncu, rows_cap, hist, &rtotal);
+    return;
+  }
+  if (t != 0) return;
+  const uint32_t Lu = max(L0, v3::kMinCut);            // k_pkt_plan's uniform header
+  const uint32_t Lb = Lu + Lu / 8u;
+  const uint32_t E0 = q0.x > (1 << 21) ? 0xFFFFFFFFu : (uint32_t)q0.x * 8u + 6u;
+  const uint32_t n0 = v3::seg_count(E0, cols_of(q0.y, q0.z), Lb, v3::kMinCut);
+  nrows[v3::kPlanRows] = (int32_t)min((uint32_t)npkts * n0, (uint32_t)rows_cap);
+  nrows[v3::kPlanFixes] = 0;
+  nrows[v3::kPlanUniform] = (int32_t)n0;
+  nrows[v3::kPlanDropped] = (uint32_t)npkts * n0 > (uint32_t)rows_cap ? (int32_t)((uint32_t)npkts * n0 - rows_cap) : 0;
+  nrows[v3::kPlanNcu] = ncu;
+  nrows[v3::kPlanExpLen] = q0.x; nrows[v3::kPlanExpCr] = q0.y;
+  nrows[v3::kPlanExpSoft] = q0.z; nrows[v3::kPlanExpMod] = q0.w;
+  nrows[v3::kPlanExpN] = npkts;
+}
+
 // The second half of a split plan (rx chain): the mixed batch's sort and row expansion, on a
 // side stream forked right after k_signal_vit, so it runs beside k_pkt_plan and k_data_fft
 // (one block of 1024 threads: config 5's takes ~140 us, longer than k_data_fft alone).  It
@@ -591,7 +766,8 @@ __global__ __launch_bounds__(1024) void k_pkt_rows(const int32_t* __restrict__ v
 // groups of ds_write_b128 hit 8 slots), then 18 store instructions each take 64 consecutive
 // units of the wave's rows, (s, q) = divmod(64j + lane, 18): 1 KiB runs.  A wave never waits
 // on another: LDS is in order within a wave, so there are no barriers.  (Tried and dropped,
-// symbol loads by LDS-DMA, with and without a one-iteration prefetch; soft rows
+// PERFLOG.md: symbol loads by LDS-DMA, with and without a one-iteration prefetch; the next
+// iteration's symbol prefetched into registers (233 VGPRs, 0.102 -> 0.110 ms); soft rows
 // stored by each lane.)
 #ifndef ZRX_DF_WAVES
 #define ZRX_DF_WAVES 4

@@ -171,7 +171,7 @@ inline bool static_storage(const void* p, size_t n, uintptr_t* s_out, uintptr_t*
 // that a new array overlaps without containing it is dropped first.
 class HostRegistry {
  public:
-  static constexpr size_t kMinRegister = size_t(256) << 10;
+  static constexpr size_t kMinRegister = size_t(32) << 10;
   static constexpr int kMaxEntries = 64;
   static constexpr size_t kMaxBytes = size_t(64) << 30;
 

@@ -156,6 +156,13 @@ __device__ __forceinline__ void make_consts(Consts& K, uint32_t l, uint32_t rib)
     }
   }
   // (the lane's other positions are at lane-uniform offsets from these: snap_delta)
+#if defined(ZRX_EXPERIMENTS) && defined(ZRX_SNAP_SHARE)
+  // (timing experiment, wrong output: rows 2 and 3 of each 32-lane half store their snapshots
+  // over rows 0 and 1's, so no two rows of a half store to one bank at different addresses --
+  // the snapshot stores' only bank conflicts -- with the same instructions and addresses in
+  // bounds: does the kernel get faster without those conflicts?)
+  rib &= ~2u;
+#endif
 #pragma unroll
   for (int k = 0; k < 3; k++) K.sa[k] = rib * 64u + rev6(rotl6(pos_of(l, 0, 0), 2 * k));
 }

@@ -209,7 +209,7 @@ def node_stats():
 
 def set_host_register(mode):
     """0 = never page-lock caller arrays, 1 = the main program's static arrays (default), 2 =
-    also other arrays >= 256 KiB (the caller keeps them mapped until mode 0 or 1)."""
+    also other arrays >= 32 KiB (the caller keeps them mapped until mode 0 or 1)."""
     rc = lib().zrx_set_host_register(int(mode))
     if rc < 0:
         raise ZiriaRxError(f"zrx_set_host_register failed ({rc})")
