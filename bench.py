@@ -50,17 +50,39 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
 PIPELINE_BELOW = 8192
 
 
-def traffic_for(kernel, npkts):
-    """HBM bytes per launch of `kernel` from the committed PMC summary of the same workload
-    and the same kernel sources (csrc_sha256, ziria_amd.build.source_hash); None otherwise."""
+def pmc_kernel(kernel, npkts):
+    """The committed PMC summary's entry for `kernel` when it was measured on the same
+    workload and the same kernel sources (csrc_sha256, ziria_amd.build.source_hash); None
+    otherwise."""
     try:
         s = json.load(open(PMC_SUMMARY))
-        k = s["kernels"][kernel]
         if int(s.get("npkts", -1)) != npkts or s.get("csrc_sha256") != source_hash():
             return None
-        return k.get("hbm_bytes_per_launch")
+        return s["kernels"][kernel]
     except (OSError, KeyError, ValueError, TypeError):
         return None
+
+
+def traffic_for(kernel, npkts):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (pmc_kernel)."""
+    k = pmc_kernel(kernel, npkts)
+    return k.get("hbm_bytes_per_launch") if k else None
+
+
+def rocprof_frac(kernel, npkts, work, peak):
+    """The roofline fraction priced on the rocprofv3 kernel trace of the same sources (the
+    summary's mean launch duration, clock-ramp launches included, and its median), beside the
+    bench's own HIP-event figure: work / duration / peak."""
+    k = pmc_kernel(kernel, npkts)
+    if not k or not k.get("avg_duration_ns"):
+        return None
+    out = {"avg_duration_ms": round(k["avg_duration_ns"] / 1e6, 4),
+           "frac_avg": round(work / (k["avg_duration_ns"] * 1e-9) / peak, 4),
+           "source": "profiles/pmc_summary.json (rocprofv3 --kernel-trace of the same sources)"}
+    if k.get("median_duration_ns"):
+        out["median_duration_ms"] = round(k["median_duration_ns"] / 1e6, 4)
+        out["frac_median"] = round(work / (k["median_duration_ns"] * 1e-9) / peak, 4)
+    return out
 
 
 def main():
@@ -341,12 +363,15 @@ def rx_run(args, total, world, rank, local, dev):
                      "achieved": round(achieved_tops, 3), "peak": round(VALU_PEAK_TOPS, 1),
                      "unit": "Tops/s", "frac": round(achieved_tops / VALU_PEAK_TOPS, 4),
                      "traffic": None if args.eq else traffic_for("k_viterbi3", n),
-                     "units": f"{OPS_PER_DECODED_BIT} int ops per decoded bit x {decoded_bits} bits/launch"},
+                     "units": f"{OPS_PER_DECODED_BIT} int ops per decoded bit x {decoded_bits} bits/launch",
+                     "rocprof": None if args.eq else rocprof_frac("k_viterbi3", n, OPS_PER_DECODED_BIT * decoded_bits,
+                                                                  VALU_PEAK_TOPS * 1e12)},
         "roofline_fft": {"kernel": "k_data_fft (FFT64+GetData+demap+deinterleave)", "bound": "hbm",
                          "achieved": round(fft_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(fft_gbs / HBM_PEAK_GBS, 4),
                          "traffic": None if args.eq else traffic_for("k_data_fft", n),
-                         "units": f"544 B per data symbol x {n * nsym_data} symbols/launch"},
+                         "units": f"544 B per data symbol x {n * nsym_data} symbols/launch",
+                         "rocprof": None if args.eq else rocprof_frac("k_data_fft", n, fft_bytes, HBM_PEAK_GBS * 1e9)},
         "gather_ms": round(res["gather_s"] * 1e3, 3),
         "step_stats": step_stats,
         "step_stats_one_engine": step_stats_one,
@@ -382,6 +407,9 @@ def sub_results(args, dev):
     GPU).  The same --steps / --warmup; no CPU baselines (the headline carries its own)."""
     out = {}
     a = argparse.Namespace(**vars(args))
+    # (at least 100 timed steps for the sub-millisecond workloads: a timed region of a few ms
+    # would read a one-off host or clock hiccup as a throughput change; config 5 at least 40)
+    a.steps = max(args.steps, 100)
     t0 = time.perf_counter()
     keep = ("value", "unit", "ms_per_step", "value_one_engine", "bit_exact_check", "stage_ms", "step_stats",
             "pipeline", "config")
@@ -389,7 +417,7 @@ def sub_results(args, dev):
     r = bench_viterbi_only(a, emit=False, cpu=False)
     out["config2"] = {k: r[k] for k in keep if k in r}
     torch.cuda.empty_cache()
-    r = bench_mixed(a, emit=False, cpu=False)
+    r = bench_mixed(argparse.Namespace(**dict(vars(a), steps=max(args.steps, 40))), emit=False, cpu=False)
     out["config5"] = {k: r[k] for k in keep if k in r}
     torch.cuda.empty_cache()
     for g in (8, 4):                                    # (2048 / 4096 packets at config 3's 16384)
@@ -460,6 +488,7 @@ class StepClock:
                                 "mean": q(g, np.mean)},
                 "host_issue_ms": {"median": q(h, np.median), "max": q(h, np.max)},
                 "slowest_step": int(np.argmax(g)) if len(g) else None,
+                "gpu_steps_ms": [round(float(x), 4) for x in g],
                 "how": "HIP event after each timed step on its stream; gaps between consecutive completions"}
 
 

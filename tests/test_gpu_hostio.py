@@ -135,3 +135,40 @@ def test_wifi_rx_eq_batch_chunked():
     assert (info == info_d).all()
     ok = info[:, 4] == 1
     assert (pay[ok, :1500] == pay_d[ok, :1500]).all() and (pay[ok, :1500] == b["payload"][ok]).all()
+
+
+@pytest.mark.parametrize("shards", [1, 3])
+def test_wifi_rx_batch_chunked_mixed(shards):
+    """A mixed batch through the chunked pipeline: 3000 distinct config-5 packets
+    (8 MCS, PSDU 64..4095 B; ~110 MB of symbols: several chunks whose widest payload `cw` and
+    longest packet differ chunk to chunk, the split plan's hint read across chunks), pageable
+    arrays, on one and on three shards of GPU 0, against the device API on the same packets."""
+    import ziria_amd as Z
+    m = txgen.make_mixed_fast(3000, min_len=64, max_len=4095, sigma=3.0, seed=0xC4C4, device="cuda")
+    n, S = 3000, m["max_nsym"]
+    e = RxEngine(0)
+    e.reserve(n, S)
+    pay_d, info_d = e.rx(m["sym"], m["sym_off"], m["nsym"], S)
+    torch.cuda.synchronize()
+    e.close()
+    pay_d, info_d = pay_d.cpu().numpy(), info_d.cpu().numpy()
+    off, ns = m["sym_off"].cpu().numpy(), m["nsym"].cpu().numpy()
+    sym = m["sym"].cpu().numpy()
+    idx = np.concatenate([np.arange(o, o + k) for o, k in zip(off, ns)])
+    sym = np.ascontiguousarray(sym[idx])
+    csr = np.concatenate([[0], np.cumsum(ns)]).astype(np.int32)
+    assert sym.nbytes > 3 * (32 << 20)                      # (more than three chunks)
+    pay = np.full((n, 4096), 0xA5, np.uint8)
+    info = np.zeros((n, 8), np.int32)
+    try:
+        if shards > 1:
+            Z.set_devices([0] * shards, 0)
+        rc = lib().__ext_wifi_rx_batch(_p(sym), sym.shape[0], _p(csr), n + 1, _p(pay), n * 4096 * 8, _p(info), n * 8)
+        assert Z.node_stats()["last_shards"] == shards
+    finally:
+        Z.set_devices(None, -1)
+    assert rc == int((info_d[:, 4] == 1).sum()) > n // 3
+    assert (info == info_d).all()
+    for i in range(n):
+        L = max(int(info[i, 2]) - 4, 0) if info[i, 4] else 0
+        assert (pay[i, :L] == pay_d[i, :L]).all(), i

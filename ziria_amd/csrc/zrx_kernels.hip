@@ -557,11 +557,25 @@ __global__ __launch_bounds__(1024) void k_pkt_plan(const int32_t* __restrict__ v
 // batch's rows (plan_rows_mixed) unless k_pkt_rows does them beside k_data_fft (split).
 // nrows null: offsets only.
 constexpr int kPsThreads = 1024, kPsPer = 4, kPsBlock = kPsThreads * kPsPer;
+// A block's record: three self-validating words, each {epoch, value} written by one 64-bit
+// relaxed atomic store and read by relaxed atomic loads (which the memory model keeps coherent
+// across the XCDs' L2s) until the epoch matches, so no release / acquire fence is needed (an
+// agent-scope fence writes back or invalidates the XCD's whole L2).
 struct PlanScanRec {
-  uint32_t u, s;            // the block's 256-B soft units, data symbols
-  unsigned long long cols;  // its trellis columns
-  uint32_t same, ready;     // all its packets equal to packet 0; == epoch once published
+  unsigned long long wu, ws, wc;   // epoch << 32 | 256-B soft units; | data symbols; | same << 31 | columns
 };
+__device__ __forceinline__ unsigned long long ps_load(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ps_store(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// spin until a record word carries this launch's epoch; its value
+__device__ __forceinline__ uint32_t ps_wait(const unsigned long long* p, uint32_t epoch) {
+  unsigned long long v;
+  while ((uint32_t)((v = ps_load(p)) >> 32) != epoch) __builtin_amdgcn_s_sleep(1);
+  return (uint32_t)v;
+}
 __global__ __launch_bounds__(kPsThreads) void k_pkt_scan(const int32_t* __restrict__ vparams, int npkts,
                                                          int64_t* __restrict__ off, int32_t* __restrict__ dsym,
                                                          int32_t* __restrict__ wave_p0, int2* __restrict__ rows,
@@ -620,21 +634,19 @@ __global__ __launch_bounds__(kPsThreads) void k_pkt_scan(const int32_t* __restri
     uint32_t bu = 0, bs = 0, bf = 1;
     unsigned long long bc = 0;
     for (int w = 0; w < kW; w++) { bu += wsum_u[w]; bs += wsum_s[w]; bc += wcols[w]; bf &= wflag[w]; }
-    rec[b].u = bu;
-    rec[b].s = bs;
-    rec[b].cols = bc;
-    rec[b].same = bf;
-    __hip_atomic_store(&rec[b].ready, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long e = (unsigned long long)epoch << 32;
+    ps_store(&rec[b].wu, e | bu);
+    ps_store(&rec[b].ws, e | bs);
+    // (a block's columns: at most 4096 x 16406 < 2^31)
+    ps_store(&rec[b].wc, e | ((unsigned long long)bf << 31) | (bc & 0x7FFFFFFFull));
   }
   if (wv == 0) {                                       // every earlier block's sums
     uint32_t au = 0, as = 0;
     for (int j0 = 0; j0 < b; j0 += 64) {
       const int j = j0 + lane;
       if (j < b) {
-        while (__hip_atomic_load(&rec[j].ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != epoch)
-          __builtin_amdgcn_s_sleep(1);
-        au += rec[j].u;
-        as += rec[j].s;
+        au += ps_wait(&rec[j].wu, epoch);
+        as += ps_wait(&rec[j].ws, epoch);
       }
     }
     for (int o = 32; o > 0; o >>= 1) {
@@ -657,22 +669,21 @@ __global__ __launch_bounds__(kPsThreads) void k_pkt_scan(const int32_t* __restri
     u0 += vu[i];
     s0 += vs[i];
   }
-  // the last block to get here reduces the records: the batch's totals and its verdict
-  __syncthreads();
+  // the last block to get here reduces the records (each read as its epoch shows it): the
+  // batch's totals and its verdict
   if (t == 0) {
-    __threadfence();
-    last = atomicAdd(ctr, 1u) == (uint32_t)nb - 1u;
-    if (last) *ctr = 0u;                               // (ready for the next launch on this stream)
+    last = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)nb - 1u;
+    if (last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // (for the next launch)
   }
   __syncthreads();
   if (!last) return;
-  __threadfence();
   uint64_t tc = 0;
   uint32_t ts = 0, all_same = 1;
   for (int j = t; j < nb; j += kPsThreads) {
-    tc += rec[j].cols;
-    ts += rec[j].s;
-    all_same &= rec[j].same;
+    const uint32_t c = ps_wait(&rec[j].wc, epoch);
+    tc += c & 0x7FFFFFFFu;
+    all_same &= c >> 31;
+    ts += ps_wait(&rec[j].ws, epoch);
   }
   for (int o = 32; o > 0; o >>= 1) {
     tc += (uint64_t)__shfl_xor((long long)tc, o);
