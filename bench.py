@@ -127,9 +127,9 @@ def main():
     if args.config == 1:
         return bench_capture(args)
     if args.config == 2:
-        return bench_viterbi_only(args)
+        return bench_viterbi_only(args, cpu=not args.no_cpu)
     if args.config == 5:
-        return bench_mixed(args)
+        return bench_mixed(args, cpu=not args.no_cpu)
 
     world = int(os.environ.get("WORLD_SIZE", "0"))
     if args.gpus > 1 and world == 0:
@@ -403,31 +403,42 @@ def rank_devices(dev, rank_elapsed, local):
 def sub_results(args, dev):
     """The secondary workloads on the same GPU, each with its own timing and bit-exact check,
     for the driver's one-GPU line: BASELINE config 2 (batched Viterbi alone), config 5 (mixed
-    MCS), and config 4's shard sizes at 4 and 8 GPUs (2048 / 4096 packets of config 3 on one
-    GPU).  The same --steps / --warmup; no CPU baselines (the headline carries its own)."""
+    MCS), and config 4's shard sizes at 8 and 4 GPUs (2048 / 4096 packets of config 3 on one
+    GPU).  Each runs as its own child process (this script again, no exec), as it does
+    standalone: in one process the streams of the workloads before it would share the
+    process's few hardware queues with its own, and two batches in flight would serialize
+    (config 5: 94.7 in-process against 108-109 Gbit/s).  No CPU baselines (the headline
+    carries its own)."""
+    import subprocess
     out = {}
-    a = argparse.Namespace(**vars(args))
-    # (at least 100 timed steps for the sub-millisecond workloads: a timed region of a few ms
-    # would read a one-off host or clock hiccup as a throughput change; config 5 at least 40)
-    a.steps = max(args.steps, 100)
     t0 = time.perf_counter()
     keep = ("value", "unit", "ms_per_step", "value_one_engine", "bit_exact_check", "stage_ms", "step_stats",
             "pipeline", "config")
-    torch.cuda.empty_cache()                            # (each workload allocates afresh)
-    r = bench_viterbi_only(a, emit=False, cpu=False)
-    out["config2"] = {k: r[k] for k in keep if k in r}
-    torch.cuda.empty_cache()
-    r = bench_mixed(argparse.Namespace(**dict(vars(a), steps=max(args.steps, 40))), emit=False, cpu=False)
-    out["config5"] = {k: r[k] for k in keep if k in r}
-    torch.cuda.empty_cache()
+    # (at least 100 timed steps for the sub-millisecond workloads: a timed region of a few ms
+    # would read a one-off host or clock hiccup as a throughput change; config 5 at least 40)
+    steps = str(max(args.steps, 100))
+    common = ["--warmup", str(args.warmup), "--batches", str(args.batches), "--no-cpu", "--no-sub"]
+    jobs = [("config2", ["--config", "2", "--steps", steps, "--payload", str(args.payload),
+                         "--npkts", str(args.npkts)], None),
+            ("config5", ["--config", "5", "--steps", str(max(args.steps, 40)), "--npkts", str(args.npkts)], None)]
     for g in (8, 4):                                    # (2048 / 4096 packets at config 3's 16384)
         n = max(1, args.npkts // g)
-        r = rx_run(a, n, 1, 0, dev.index or 0, dev)
-        r.pop("batch0", None)
-        out[f"shard_{n}"] = dict({k: r[k] for k in keep if k in r}, unit="Mbit/s",
-                                 step_stats_one_engine=r["step_stats_one_engine"],
-                                 what=f"config 4's per-GPU shard at {g} GPUs: {n} config-3 packets")
-        torch.cuda.empty_cache()
+        jobs.append((f"shard_{n}", ["--npkts", str(n), "--steps", steps, "--payload", str(args.payload)],
+                     f"config 4's per-GPU shard at {g} GPUs: {n} config-3 packets"))
+    for name, extra, what in jobs:
+        cmd = [sys.executable, os.path.abspath(sys.argv[0])] + extra + common
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=400)
+        lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+        if p.returncode != 0 or not lines:
+            out[name] = {"error": f"exit {p.returncode}", "stderr_tail": p.stderr[-800:]}
+            continue
+        r = json.loads(lines[-1])
+        out[name] = {k: r[k] for k in keep if k in r}
+        if "step_stats_one_engine" in r:
+            out[name]["step_stats_one_engine"] = r["step_stats_one_engine"]
+        if what:
+            out[name]["what"] = what
+        out[name]["command"] = "bench.py " + " ".join(extra + common)
     out["wall_s"] = round(time.perf_counter() - t0, 1)
     return out
 
@@ -585,6 +596,8 @@ def bench_viterbi_only(args, emit=True, cpu=True):
     for e in engs:
         e.close()
     if not cpu:
+        if emit:
+            print(json.dumps(line), flush=True)
         return line
     # CPU port (AVX-512 brick loop, identical to the oracle) on every allowed core, chunks of
     # the same frames for about --cpu-seconds

@@ -244,6 +244,7 @@ def test_bench_default_line_carries_sub_results(oracle, tmp_path):
         b = sub[k]["bit_exact_check"]
         assert b["payload_match"] is True and b["mismatched_packets"] == 0 and b["packets"] == 2 * int(k[6:])
     for k in ("config2", "config5", "shard_4", "shard_8"):
+        assert "error" not in sub[k] and sub[k]["command"].startswith("bench.py ")     # (its own child process)
         assert sub[k]["ms_per_step"] > 0 and sub[k]["value"] > 0
         g = sub[k]["step_stats"]["gpu_step_ms"]
         assert g["min"] <= g["median"] <= g["max"]
