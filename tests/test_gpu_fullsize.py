@@ -82,3 +82,31 @@ def test_fullsize_eq_bench_batches_vs_port(oracle, seed):
     ok = crc == 1
     assert 16000 < ok.sum() < 16384
     assert (pay[ok, :1500] == b["payload"][ok]).all()
+
+
+def test_mixed_noise_packed_plan_vs_port(oracle):
+    """A mixed batch large enough for the packed plan (zrx_kernels.hip plan_waves_fill), with
+    every fourth packet's data symbols replaced by noise: those frames decode to garbage, their
+    segments' warm-ups need not converge, and the seam pass re-decodes from the seams whose
+    two sides disagree (table geometry).  Every packet against the port, bit for bit."""
+    m = txgen.make_mixed_fast(4096, min_len=64, max_len=2048, sigma=3.0, seed=0x5EA4, device="cuda")
+    sym = m["sym"].clone()
+    g = torch.Generator(device="cuda")
+    g.manual_seed(7)
+    off, ns = m["sym_off"].cpu().numpy(), m["nsym"].cpu().numpy()
+    for i in range(0, 4096, 4):
+        a, n = int(off[i]) + 1, int(ns[i]) - 1          # (the SIGNAL symbol stays: a valid header)
+        if n > 0:
+            sym[a:a + n] = torch.randint(-3000, 3000, (n, 64, 2), generator=g, device="cuda", dtype=torch.int16)
+    b = dict(m, sym=sym)
+    e = RxEngine(0)
+    e.reserve(4096, m["max_nsym"])
+    e.rx(sym, m["sym_off"], m["nsym"], m["max_nsym"])
+    torch.cuda.synchronize()
+    hdr = e.plan_dump(4096)["header"]
+    rows, fixes = e.plan_stats()
+    e.close()
+    assert hdr[6] == 1                                       # the packed plan
+    crc, _ = _check(oracle, b)
+    print(f"crc pass {crc.sum()} of 4096, seam fixes {fixes}")
+    assert 2000 < crc.sum() < 3200 and fixes > 0
