@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round-6 evidence session on the final sources: the GPU parity suite and smoke(), the default
 # bench line (headline + sub-results), --e2e, --eq, --tx, --config 1, then the rocprof kernel
-# trace and PMC passes of the headline (scripts/gpu_pmc.sh -> gpurun_out/pmc_summary.json).
+# trace and PMC passes of the headline (scripts/gpu_pmc.sh -> gpurun_out/pmc_summary.json), and
+# the kernel trace of config 5 on one engine.
 # Outputs go to gpurun_out/final_*; copy what is judged into profiles/r06/.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 step() { echo "== $1 $(date +%T)"; }
@@ -33,5 +34,13 @@ if [ -z "$SKIP_PMC" ]; then
   ./scripts/gpu_pmc.sh > gpurun_out/final_pmc.log 2>&1; rc=$?
   echo "pmc rc=$rc"; tail -3 gpurun_out/final_pmc.log; [ $rc -eq 0 ] || exit $rc
   python scripts/kstats.py gpurun_out/prof/run_kernel_stats.csv
+fi
+if [ -z "$SKIP_C5PROF" ]; then
+  step c5prof
+  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+     -d "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/c5prof" -o c5 -- python3 "${GRAFT_REPO_ROOT:-/root/repo}/bench.py" \
+     --config 5 --pipeline 1 --steps 20 --warmup 5 --no-cpu --no-sub > "${GRAFT_REPO_ROOT:-/root/repo}/gpurun_out/final_c5prof.log" 2>&1); rc=$?
+  echo "c5prof rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  python scripts/kstats.py gpurun_out/c5prof/c5_kernel_stats.csv
 fi
 exit 0

@@ -750,9 +750,6 @@ __device__ __forceinline__ void traceback(bool due, const uint32_t (&M)[kDw], ui
     walker = due && l == 0 && cnt != 0;
     wm = __builtin_amdgcn_ballot_w64(walker);
     if (wm == 0) return;
-#ifdef ZRX_NO_FINAL_WALK
-    if (!DEFER) return;                                // (timing probe: the argmin without the walk)
-#endif
     s0 = ((uint32_t)kb >> 2) & 63u;
     // the winner's half q in its lane: q = rotr6(s0 ^ st0, ph) < 8 (position bits 0..2);
     // the row's 8 pad bytes in byte order q, one v_perm picks it, the other lanes give 0
@@ -1753,7 +1750,9 @@ __device__ __forceinline__ void viterbi_rows_packed(int g0, int nrows, uint32_t 
   const uint32_t rib = threadIdx.x >> v3::kLaneBits;
   const int slot = g0 + (int)rib;
   const bool valid = slot < nrows;
-  const uint32_t w = (uint32_t)slot >> 3, j = (uint32_t)slot & 7u;   // (a wave's rows: slots 8w .. 8w + 7)
+  // (a wave's rows: slots 8w .. 8w + 7.  Placing a CU's 8 waves on consecutive waves of the
+  // plan, so that they share a rate and its code, measured the same: PERFLOG round 6.)
+  const uint32_t w = (uint32_t)slot >> 3, j = (uint32_t)slot & 7u;
   const uint32_t i0 = valid ? 8u * (uint32_t)P.rfirst[w] + j : 0u, i1 = valid ? 8u * (uint32_t)P.rfirst[w + 1] + j : 0u;
   const int cr = !valid ? -1 : w < P.wave1 ? 0 : w < P.wave2 ? 1 : 2;   // (the waves of a rate are consecutive)
   const bool younger = v3::kPrioMode != 2 && ((blockIdx.x / ncu) & 1u) != 0u;
