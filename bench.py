@@ -638,17 +638,13 @@ def bench_mixed(args, emit=True, cpu=True):
           for j in range(nb)]
     gen_s = time.perf_counter() - tg
     S = max(m["max_nsym"] for m in ms)
-    # args.pipeline engines (own workspace and stream; auto: 1 with the packed plan, else 2) take the steps in turn, as in main(),
+    # args.pipeline engines (own workspace and stream; auto: 2) take the steps in turn, as in main(),
     # linked in mode 4 by default: each batch's head (SIGNAL, plan, data FFT) on a lowest-priority
     # stream, so the other batch's Viterbi blocks (two block rounds on a mixed batch) are dispatched
     # first.  Interleaved on one box (profiles/r04q_config5_pipeline.txt): one engine 94.6-95.0
     # Gbit/s, two unlinked 75.6-90.3 (the head's blocks took CU room from the Viterbi's second
     # round), two in mode 4 101.3-101.6.
-    # With the packed plan of a mixed batch (ZRX_FILL, default on) the Viterbi's waves are all
-    # about as long, so no CU frees early for the other batch's head, whose blocks then delay
-    # whole waves of this one (two engines 80 Gbit/s against 105 for one): one engine.
-    packed = os.environ.get("ZRX_FILL", "1") != "0"
-    engs = [RxEngine(0) for _ in range(args.pipeline or (1 if packed else 2))]
+    engs = [RxEngine(0) for _ in range(args.pipeline or 2)]
     streams = [torch.cuda.Stream(dev) for _ in engs]
     link = 4 if args.link < 0 else args.link
     if len(engs) == 2 and link > 0:

@@ -218,16 +218,6 @@ int zrx_plan_stats(zrx_ctx* ctx, int32_t* stats2);
 /* ZRX_OK, or ZRX_EPLAN if the last plan dropped rows past the bound its workspace was sized
  * for (those packets would be left undecoded; never expected).  Synchronizes. */
 int zrx_plan_check(zrx_ctx* ctx);
-/* The last plan itself, for tests (synchronizes).  header16: the 16 plan header words
- * (rows, seam fixes, segments of a uniform batch, CUs, -, dropped, packed, ..., the first waves
- * of rates 1 and 2 in [14], [15]).  For a packed plan (header16[6] = 1, a mixed rx-chain batch)
- * of W = rows / 8 waves: wave w decodes parts wfirst[w] .. wfirst[w + 1] - 1 in turn, its row
- * j taking item 8 i + j of part i, item i = {packet items[2i] (-1: none), segment k | nseg << 8
- * in items[2i + 1]}; packet p's seams are at columns 256 cuts[7p + k - 1], k = 1 .. segs[p] - 1.
- * Copies at most cap_items items, cap_waves + 1 wave starts and cap_pkts packets' segs and
- * cuts; any pointer but header16 may be null. */
-int zrx_plan_dump(zrx_ctx* ctx, int32_t* header16, int32_t* items, int cap_items, int32_t* wfirst, int cap_waves,
-                  uint8_t* segs, uint16_t* cuts, int cap_pkts);
 
 /* Full chain; d_sym_off: int64 symbol index of each packet's SIGNAL symbol; d_nsym: int32
  * symbols available per packet; max_nsym: the largest d_nsym, which must fit the reserved

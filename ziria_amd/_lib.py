@@ -44,7 +44,6 @@ SIGNATURES = [
     ("zrx_viterbi_dev", C.c_int, [_P, _P, _P, _P, C.c_int, _P, _P, _P]),
     ("zrx_plan_stats", C.c_int, [_P, _P]),
     ("zrx_plan_check", C.c_int, [_P]),
-    ("zrx_plan_dump", C.c_int, [_P, _P, _P, C.c_int, _P, C.c_int, _P, _P, C.c_int]),
     ("zrx_pipeline_link", C.c_int, [_P, _P, C.c_int]),
     ("zrx_rx_dev", C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, _P, _P]),
     ("zrx_rx_eq_dev", C.c_int, [_P, _P, _P, _P, C.c_int, C.c_int, _P, _P, _P]),

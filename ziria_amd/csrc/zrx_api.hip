@@ -69,14 +69,11 @@ struct zrx_ctx {
   uint8_t* segs = nullptr;        // segments per packet
   int32_t* order = nullptr;       // k_pkt_plan scratch: packets in row order
   uint2* dumps = nullptr;         // seam metric dumps, v3::seam_index
-  int32_t* rfirst = nullptr;      // a packed plan's wave starts (plan_waves_fill)
-  uint16_t* cuts = nullptr;       // a packed plan's seams, v3::kCutsPerPkt per packet
   PlanScanRec* scan_rec = nullptr; // k_pkt_scan's per-block records (ceil(npkts / 4096) + 1)
   uint32_t* scan_ctr = nullptr;   // its finished-block counter (reset by the last block)
   uint32_t scan_epoch = 0;        // its ready mark, one per launch (never 0: records start zeroed)
   int64_t rows_cap = 0;
   bool use_order = true;          // ZRX_ORDER=0 (experiment builds) turns the plan off
-  bool fill = true;               // ZRX_FILL=0: a mixed rx-chain batch gets rows of whole frames and even segments
   // The workspace is shared by every launch of this context: a launch on a different stream
   // than the previous one first waits for the previous launch's work (ws_free).
   hipEvent_t ws_free = nullptr;
@@ -132,14 +129,13 @@ static int check_device(int device) {
 static void free_ws(zrx_ctx* c) {
   for (void* p : {(void*)c->sig_soft, (void*)c->vparams, (void*)c->soft, (void*)c->soft_off, (void*)c->dsym,
                   (void*)c->wave_p0, (void*)c->dec, (void*)c->dec_off, (void*)c->dec_bits, (void*)c->rows,
-                  (void*)c->nrows, (void*)c->segs, (void*)c->dumps, (void*)c->order, (void*)c->rfirst, (void*)c->cuts, (void*)c->scan_rec,
+                  (void*)c->nrows, (void*)c->segs, (void*)c->dumps, (void*)c->order, (void*)c->scan_rec,
                   (void*)c->scan_ctr})
     (void)hipFree(p);
   c->scan_rec = nullptr; c->scan_ctr = nullptr;
   c->sig_soft = nullptr; c->vparams = nullptr; c->soft = nullptr; c->soft_off = nullptr;
   c->dsym = nullptr; c->wave_p0 = nullptr; c->dec = nullptr; c->dec_off = nullptr; c->dec_bits = nullptr;
   c->rows = nullptr; c->nrows = nullptr; c->segs = nullptr; c->dumps = nullptr; c->order = nullptr; c->rows_cap = 0;
-  c->rfirst = nullptr; c->cuts = nullptr;
   c->cap_pkts = c->cap_nsym = 0;
 }
 
@@ -377,18 +373,18 @@ static void launch_viterbi(zrx_ctx* c, const uint8_t* soft, const int64_t* soft_
 #ifdef ZRX_EXPERIMENTS
   switch (c->v3dbg) {   // timing experiments (ZRX_V3DBG); 0 is the product kernel
 #define ZRX_V3(D) case D: k_viterbi3<D><<<g, b, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits, rows, nrows, nullptr, c->dumps); return;
-    ZRX_V3(1) ZRX_V3(2) ZRX_V3(4) ZRX_V3(8) ZRX_V3(16) ZRX_V3(64) ZRX_V3(1024) ZRX_V3(1032) ZRX_V3(2048) ZRX_V3(4096)
+    ZRX_V3(1) ZRX_V3(2) ZRX_V3(4) ZRX_V3(8) ZRX_V3(16) ZRX_V3(64) ZRX_V3(1024) ZRX_V3(1032) ZRX_V3(2048)
 #undef ZRX_V3
     default: break;
   }
 #endif
   k_viterbi3<0><<<g, b, 0, c->stream>>>(soft, soft_off, params, npkts, out, out_off, out_bits, rows, nrows, nullptr,
-                                        c->dumps, c->rfirst, c->cuts);
+                                        c->dumps);
   // the seam pass: packets whose segments disagree at a seam are re-decoded from there
   // (normally none; a block-stride grid of at most 2 blocks per CU)
   if (plan)
     k_viterbi3<0, true><<<std::min(blocks(npkts, v3::kRows), 2 * c->ncu), b, 0, c->stream>>>(
-        soft, soft_off, params, npkts, out, out_off, out_bits, nullptr, c->nrows, c->segs, c->dumps, c->rfirst, c->cuts);
+        soft, soft_off, params, npkts, out, out_off, out_bits, nullptr, c->nrows, c->segs, c->dumps);
 }
 
 // ---- FFTSafe<N> plans (zrx_fftplan.hpp), uploaded once per context --------------------
@@ -439,7 +435,6 @@ int zrx_create(zrx_ctx** out, int device, void* stream) {
   c->df_blocks = std::max(1, occ) * c->ncu;
   ZRX_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_data_fft<true>, kDfThreads, 0));
   c->df_blocks_eq = std::max(1, occ) * c->ncu;
-  if (const char* v = std::getenv("ZRX_FILL")) c->fill = std::atoi(v) != 0;
 #ifdef ZRX_EXPERIMENTS
   if (const char* v = std::getenv("ZRX_V3DBG")) c->v3dbg = std::atoi(v);
   if (const char* v = std::getenv("ZRX_ORDER")) c->use_order = std::atoi(v) != 0;
@@ -577,8 +572,6 @@ int zrx_reserve(zrx_ctx* c, int npkts, int max_nsym) {
   ZRX_CHECK(hipMalloc(&c->segs, (size_t)np + 16));
   ZRX_CHECK(hipMalloc(&c->order, (size_t)np * 4 + 16));
   ZRX_CHECK(hipMalloc(&c->dumps, (size_t)np * (v3::kMaxSeg - 1) * 2 * v3::kSeamWords * 8 + 256));
-  ZRX_CHECK(hipMalloc(&c->rfirst, (size_t)(kFillWavesMax + 8) * 4));
-  ZRX_CHECK(hipMalloc(&c->cuts, (size_t)np * v3::kCutsPerPkt * 2 + 16));
   const size_t nrec = (size_t)np / kPsBlock + 2;
   ZRX_CHECK(hipMalloc(&c->scan_rec, nrec * sizeof(PlanScanRec)));
   ZRX_CHECK(hipMalloc(&c->scan_ctr, 64));
@@ -622,23 +615,6 @@ int zrx_plan_check(zrx_ctx* c) {
     std::fprintf(stderr, "ziria_rx: the Viterbi plan dropped %d rows past its bound\n", h[v3::kPlanDropped]);
     return ZRX_EPLAN;
   }
-  return ZRX_OK;
-}
-
-int zrx_plan_dump(zrx_ctx* c, int32_t* header16, int32_t* items, int cap_items, int32_t* rfirst, int cap_rows,
-                  uint8_t* segs, uint16_t* cuts, int cap_pkts) {
-  if (!c || !header16 || cap_items < 0 || cap_rows < 0 || cap_pkts < 0) return ZRX_EINVAL;
-  std::memset(header16, 0, v3::kPlanWords * 4);
-  if (!c->nrows) return ZRX_OK;
-  zrx_shard::DeviceGuard dg(c->device);
-  ZRX_CHECK(hipStreamSynchronize(c->stream));
-  ZRX_CHECK(hipMemcpy(header16, c->nrows, v3::kPlanWords * 4, hipMemcpyDeviceToHost));
-  const int ni = (int)std::min<int64_t>(cap_items, c->rows_cap), nr = std::min(cap_rows, kFillWavesMax);
-  const int np = std::min(cap_pkts, c->cap_pkts);
-  if (items && ni > 0) ZRX_CHECK(hipMemcpy(items, c->rows, (size_t)ni * 8, hipMemcpyDeviceToHost));
-  if (rfirst && nr >= 0) ZRX_CHECK(hipMemcpy(rfirst, c->rfirst, (size_t)(nr + 1) * 4, hipMemcpyDeviceToHost));
-  if (segs && np > 0) ZRX_CHECK(hipMemcpy(segs, c->segs, (size_t)np, hipMemcpyDeviceToHost));
-  if (cuts && np > 0) ZRX_CHECK(hipMemcpy(cuts, c->cuts, (size_t)np * v3::kCutsPerPkt * 2, hipMemcpyDeviceToHost));
   return ZRX_OK;
 }
 
@@ -759,7 +735,7 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
     ZRX_CHECK(hipEventRecord(c->ev_fork, h));
     ZRX_CHECK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
     k_pkt_rows<<<1, 1024, 0, c->side>>>(c->vparams, npkts, c->rows, c->nrows, c->segs, c->order, c->dec_bits, c->ncu,
-                                        (int)plan_rows_max(c, npkts), c->fill ? c->rfirst : nullptr, c->cuts);
+                                        (int)plan_rows_max(c, npkts));
     ZRX_CHECK(hipEventRecord(c->ev_join, c->side));
   }
   // the plan: offsets, the batch verdict and (unless split) a mixed batch's rows, over many blocks
@@ -767,8 +743,7 @@ static int rx_chain(zrx_ctx* c, const struct complex16* d_sym, const int64_t* d_
   k_pkt_scan<<<blocks(npkts, kPsBlock), kPsThreads, 0, h>>>(
       c->vparams, npkts, c->soft_off, c->dsym, c->wave_p0, ordered ? c->rows : nullptr, ordered ? c->nrows : nullptr,
       c->segs, c->order, c->dec_bits, c->ncu, (int)plan_rows_max(c, npkts), split ? 1 : 0,
-      ordered ? c->mixed_hint_dev : nullptr, c->scan_rec, c->scan_ctr, c->scan_epoch, c->fill ? c->rfirst : nullptr,
-      c->cuts);
+      ordered ? c->mixed_hint_dev : nullptr, c->scan_rec, c->scan_ctr, c->scan_epoch);
   if (ev) ZRX_CHECK(hipEventRecord(ev[2], h));
   // k_data_fft: waves over the batch's data symbols, at most npkts x (max_nsym - 1) of them
   const int fft_blocks = (int)std::min<int64_t>(((int64_t)npkts * (max_nsym - 1) + kDfThreads - 1) / kDfThreads,

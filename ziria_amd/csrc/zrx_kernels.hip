@@ -410,325 +410,11 @@ __device__ __forceinline__ void plan_rows_mixed(const int32_t* __restrict__ vpar
     nrows[v3::kPlanRows] = (int32_t)min(total, (uint32_t)rows_cap);
     nrows[v3::kPlanFixes] = 0;                         // counted by the seam pass
     nrows[v3::kPlanUniform] = 0;
-    nrows[v3::kPlanPacked] = 0;
     // rows past the bound (plan_rows_max) are dropped: never by construction, but a wrong
     // bound must show (zrx_plan_check) instead of leaving packets silently undecoded
     nrows[v3::kPlanDropped] = total > (uint32_t)rows_cap ? (int32_t)(total - (uint32_t)rows_cap) : 0;
     nrows[v3::kPlanNcu] = (int32_t)ncu2;
   }
-}
-
-// ---- The packed plan of a mixed batch (rx chain) -----------------------------------------
-// Rows of whole frames or even segments leave a mixed batch's waves anywhere between a short
-// frame and 11/8 of the fair share, and k_viterbi3 lasts as long as its longest wave (config
-// 5: ~6100 columns against a mean of ~4400).  Here every wave is filled to about the same
-// length instead.  Per rate, the packets sorted by length form groups of 8 consecutive frames,
-// decoded in lockstep by the 8 rows of a wave (they start together, so their traceback windows
-// fall on the same columns and walk as one, as in a batch of whole frames); a group lasts as
-// long as its longest frame.  The groups of a rate form one stream of columns, cut into W_r
-// waves of T_r = C_r / W_r columns (at least kFillTmin), W_r in proportion to C_r and the waves
-// one block round (8 per CU).  A wave boundary w T_r inside a group becomes a seam of the
-// group there, moved to the nearest window start J (a multiple of 256 columns, 256 <= J <=
-// E - 64 of the group's longest frame) or to the group's start or end, whichever is nearest;
-// every frame of the group for which J + 64 <= E takes that seam (v3::seg_J table geometry),
-// the shorter ones end before it.  A group with m seams has m + 1 parts; a wave decodes the
-// parts between its two boundaries one after another, all 8 rows starting a part together
-// (k_viterbi3's packed rows, v3::PackCtx).
-// Writes: items (8 per part: part i's row j is items[8 i + j] = {packet, k | nseg << 8} or
-// {-1, 0} for none), wfirst[0 .. NW] (a wave's first part), segs[p], cuts[p][], out_bits[p] =
-// 0 for packets with no columns, and the plan header (kPlanPacked = 1, the first waves of rates
-// 1 and 2 in kPlanWave1 / kPlanWave2, rows = 8 NW).  One 1024-thread block; hist: kOrderPerThread
-// x 1024 words, zeroed; *rtotal zeroed.
-constexpr int kFillPer = 4;                            // groups a thread takes per round
-constexpr uint32_t kFillTmin = 2560;                   // wave stream columns at least (<= 7 seams a group)
-constexpr int kFillWavesMax = 8 * 256 + 8;             // one block round on 256 CUs (+ rounding)
-struct FillClass {
-  uint32_t start, end;                                 // sorted positions
-  uint32_t g0, ng;                                     // first group, groups
-  uint32_t ctot, a0;                                   // group-stream columns, columns before the class
-  uint32_t wb, nw;                                     // first wave, waves
-};
-// ideal boundary w of a class (group-stream coordinates)
-__device__ __forceinline__ uint64_t fill_X(const FillClass& F, uint32_t w) {
-  return (uint64_t)F.ctot >= (uint64_t)F.nw * kFillTmin ? (uint64_t)w * F.ctot / F.nw : (uint64_t)w * kFillTmin;
-}
-__device__ __forceinline__ uint32_t fill_w0(const FillClass& F, uint32_t x) {    // least w >= 1 with X(w) >= x
-  const uint64_t r = (uint64_t)F.ctot >= (uint64_t)F.nw * kFillTmin ? ((uint64_t)x * F.nw + F.ctot - 1) / F.ctot
-                                                                     : ((uint64_t)x + kFillTmin - 1) / kFillTmin;
-  return (uint32_t)max<uint64_t>(r, 1);
-}
-// the boundary nearest X within a group at stream position x (c columns, E = 8 len + 6 of its
-// longest frame): the group's start, its end, or a window start J inside it
-__device__ __forceinline__ uint32_t fill_adjust(uint32_t x, uint32_t c, uint32_t E, uint64_t X) {
-  const uint32_t xr = (uint32_t)(X - x);
-  uint32_t b = xr <= c - xr ? 0u : c;
-  if (c >= E && E <= v3::kSegMaxEnd && E >= 320u) {
-    const uint32_t jmax = (E - 64u) & ~255u;
-    const uint32_t J = min(max((xr + 128u) & ~255u, 256u), jmax);
-    if (jmax >= 256u && (J > xr ? J - xr : xr - J) < (b > xr ? b - xr : xr - b)) b = J;
-  }
-  return x + b;
-}
-__device__ __forceinline__ int fill_class(const FillClass* F, uint32_t g) {
-  return g < F[1].g0 ? 0 : g < F[2].g0 ? 1 : 2;
-}
-constexpr int kFillGroupsMax = 4096 + 8;
-constexpr int kFillMinPkts = 256;               // groups (packets / 8) the plan takes (else rows of frames)
-__device__ __forceinline__ void plan_waves_fill(const int32_t* __restrict__ vparams, int npkts, int2* __restrict__ items,
-                                                int32_t* __restrict__ nrows, uint8_t* __restrict__ segs,
-                                                int32_t* __restrict__ order, int32_t* __restrict__ out_bits, int ncu,
-                                                int rows_cap, uint32_t* hist, uint32_t* rtotal,
-                                                int32_t* __restrict__ wfirst, uint16_t* __restrict__ cuts) {
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  __shared__ uint32_t bnd[kFillWavesMax + 1];
-  __shared__ uint32_t gkey[kFillGroupsMax];            // group: longest frame's columns << 16 | its E
-  __shared__ uint32_t gx[kFillGroupsMax];              // group: stream position in its class
-  __shared__ uint32_t gpm[kFillGroupsMax];             // group: first part << 3 | seams
-  __shared__ FillClass F[3];
-  __shared__ uint32_t esum[16], csum[3], nwt;
-  plan_pkts<false>(vparams, npkts, 0u, hist, order, segs, out_bits, rtotal);   // (L = 0: one row a packet)
-  __syncthreads();
-  const uint32_t npk = order_hist_scan(hist);
-  __syncthreads();
-  plan_pkts<true>(vparams, npkts, 0u, hist, order, segs, out_bits, nullptr);
-  if (t < 3) csum[t] = 0;
-  __syncthreads();                                     // order[] sorted by (rate, length); hist[key] = bucket end
-  if (t == 0) {
-    uint32_t pos = 0, g = 0;
-    for (int r = 0; r < 3; r++) {
-      F[r].start = pos;
-      pos = hist[r * kOrderLen + kOrderLen - 1];
-      F[r].end = pos;
-      F[r].g0 = g;
-      F[r].ng = (F[r].end - F[r].start + 7u) / 8u;
-      g += F[r].ng;
-    }
-  }
-  __syncthreads();
-  const uint32_t NG = min(F[2].g0 + F[2].ng, (uint32_t)kFillGroupsMax);   // (the caller keeps npkts <= 8 x max)
-  auto cls_pos = [&](uint32_t pos) { return pos < F[0].end ? 0 : pos < F[1].end ? 1 : 2; };
-  for (uint32_t g = t; g < NG; g += 1024u) gkey[g] = 0;
-  __syncthreads();
-  // the groups' lengths: every frame's columns into its group's key (one load level a frame)
-  for (uint32_t pos = t; pos < npk; pos += 1024u) {
-    const int4 q = *reinterpret_cast<const int4*>(vparams + 4 * (int64_t)order[pos]);
-    const FillClass& C = F[cls_pos(pos)];
-    const uint32_t g = C.g0 + ((pos - C.start) >> 3);
-    if (g < NG) atomicMax(&gkey[g], (min(cols_of(q.y, q.z), 65535u) << 16) | min((uint32_t)q.x * 8u + 6u, 65535u));
-  }
-  __syncthreads();
-  {                                                    // the classes' group-stream totals
-    uint32_t my[3] = {0, 0, 0};
-    for (uint32_t g = t; g < NG; g += 1024u) my[fill_class(F, g)] += gkey[g] >> 16;
-    for (int r = 0; r < 3; r++) {
-      uint32_t v = my[r];
-      for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
-      if (lane == 0 && v) atomicAdd(&csum[r], v);
-    }
-  }
-  __syncthreads();
-  if (t == 0) {
-    uint32_t all = 0;
-    for (int r = 0; r < 3; r++) { F[r].ctot = csum[r]; F[r].a0 = all; all += csum[r]; }
-    // waves: one block round (8 per CU), T >= kFillTmin, shared out by columns
-    // (and the item list's room: 8 items a part, parts <= groups + waves)
-    const uint32_t ng = F[2].g0 + F[2].ng, room = (uint32_t)max(rows_cap, 0) / 8u;
-    const uint32_t wcap = room > ng + 4u ? room - ng - 4u : 1u;
-    const uint32_t waves = (uint32_t)min<uint64_t>(min<uint64_t>(min(8 * max(ncu, 1), kFillWavesMax - 8), wcap),
-                                                   max<uint64_t>(((uint64_t)all + kFillTmin - 1) / kFillTmin, 1));
-    uint32_t w[3], used = 0;
-    for (int r = 0; r < 3; r++) {
-      w[r] = F[r].ctot ? max((uint32_t)((uint64_t)waves * F[r].ctot / max(all, 1u)), 1u) : 0u;
-      used += w[r];
-    }
-    while (used > waves) {                             // (the max(.., 1) above can overshoot)
-      int rm = -1;
-      for (int r = 0; r < 3; r++)
-        if (w[r] > 1u && (rm < 0 || (uint64_t)F[r].ctot * w[rm] < (uint64_t)F[rm].ctot * w[r])) rm = r;
-      if (rm < 0) break;
-      w[rm]--; used--;
-    }
-    while (used < waves) {                             // leftovers to the longest waves
-      int rm = -1;
-      for (int r = 0; r < 3; r++)
-        if (w[r] && (rm < 0 || (uint64_t)F[r].ctot * w[rm] > (uint64_t)F[rm].ctot * w[r])) rm = r;
-      if (rm < 0) break;
-      w[rm]++; used++;
-    }
-    uint32_t wb = 0;
-    for (int r = 0; r < 3; r++) { F[r].wb = wb; F[r].nw = w[r]; wb += w[r]; }
-    nwt = wb;
-  }
-  __syncthreads();
-  const uint32_t NW = nwt;
-  for (int r = 0; r < 3; r++)
-    for (uint32_t w = t; w < F[r].nw; w += 1024u) {
-      bnd[F[r].wb + w] = w ? F[r].ctot : 0u;         // (waves past the stream's end stay empty)
-      wfirst[F[r].wb + w] = -1;
-    }
-  __syncthreads();
-  // over the groups in rounds: the stream positions and the boundaries each group holds, then
-  // (second sweep) its seams, parts and the waves' first parts
-  for (int sweep = 0; sweep < 2; sweep++) {
-    uint32_t carry = 0;
-    for (uint32_t base = 0; base < NG; base += 1024u * kFillPer) {
-      uint32_t v[kFillPer], sum = 0;
-#pragma unroll
-      for (int i = 0; i < kFillPer; i++) {
-        const uint32_t g = base + kFillPer * (uint32_t)t + i;
-        v[i] = 0;
-        if (g < NG) {
-          if (sweep == 0) {
-            v[i] = gkey[g] >> 16;
-          } else {                                     // parts: 1 + the distinct seams inside
-            const FillClass& C = F[fill_class(F, g)];
-            const uint32_t x = gx[g], c = gkey[g] >> 16;
-            uint32_t ncut = 0, last = x;
-            for (uint32_t w = fill_w0(C, x); w < C.nw; w++) {
-              if (fill_X(C, w) >= (uint64_t)x + c) break;
-              const uint32_t b = bnd[C.wb + w];
-              if (b > x && b < x + c && b != last) { ncut++; last = b; }
-            }
-            v[i] = 1u + ncut;
-          }
-        }
-        sum += v[i];
-      }
-      const uint32_t inc = wave_incl_scan(sum);
-      if (lane == 63) esum[wv] = inc;
-      __syncthreads();
-      uint32_t ex = carry + inc - sum, rnd = 0;
-      for (int w = 0; w < 16; w++) { ex += w < wv ? esum[w] : 0u; rnd += esum[w]; }
-      __syncthreads();                                 // esum is rewritten by the next round
-      carry += rnd;
-#pragma unroll
-      for (int i = 0; i < kFillPer; i++) {
-        const uint32_t g = base + kFillPer * (uint32_t)t + i;
-        if (g < NG) {
-          const FillClass& C = F[fill_class(F, g)];
-          const uint32_t c = gkey[g] >> 16, gE = gkey[g] & 0xFFFFu;
-          if (sweep == 0) {
-            const uint32_t x = ex - C.a0;
-            gx[g] = x;
-            uint32_t ncut = 0, last = x;
-            for (uint32_t w = fill_w0(C, x); w < C.nw; w++) {
-              const uint64_t X = fill_X(C, w);
-              if (X >= (uint64_t)x + c) break;
-              uint32_t b = fill_adjust(x, c, gE, X);
-              if (b > x && b < x + c) {                // a seam: at most kCutsPerPkt distinct ones
-                if (b == last) {
-                } else if (ncut < (uint32_t)v3::kCutsPerPkt) {
-                  ncut++; last = b;
-                } else {
-                  b = x + c;
-                }
-              }
-              bnd[C.wb + w] = b;
-            }
-          } else {
-            const uint32_t x = gx[g], m = v[i] - 1u, nex = ex;
-            gpm[g] = (nex << 3) | m;
-            if (g == C.g0) wfirst[C.wb] = (int32_t)nex;  // the class's first wave
-            uint32_t k = 0, last = x;
-            for (uint32_t w = fill_w0(C, x); w < C.nw; w++) {
-              if (fill_X(C, w) >= (uint64_t)x + c) break;
-              const uint32_t b = bnd[C.wb + w];
-              if (b > x && b < x + c && b != last) { k++; last = b; }
-              wfirst[C.wb + w] = (int32_t)(nex + (b <= x ? 0u : b >= x + c ? m + 1u : k));
-            }
-            // the rows a short last group has no frame for: nothing in every part
-            const uint32_t nf = min(8u, C.end - (C.start + 8u * (g - C.g0)));
-            for (uint32_t j = nf; j < 8u; j++)
-              for (uint32_t q = 0; q <= m; q++)
-                if (8u * (nex + q) + j < (uint32_t)rows_cap) items[8u * (nex + q) + j] = make_int2(-1, 0);
-          }
-        }
-        ex += v[i];
-      }
-    }
-    if (sweep == 1 && t == 0) *rtotal = carry;         // parts
-    __syncthreads();
-  }
-  // every frame: its seams (the prefix of its group's for which J + 64 <= E) and its items
-  for (uint32_t pos = t; pos < npk; pos += 1024u) {
-    const int32_t p = order[pos];
-    const int4 q = *reinterpret_cast<const int4*>(vparams + 4 * (int64_t)p);
-    const FillClass& C = F[cls_pos(pos)];
-    const uint32_t g = C.g0 + ((pos - C.start) >> 3), j = (pos - C.start) & 7u;
-    if (g >= NG) continue;
-    const uint32_t x = gx[g], c = gkey[g] >> 16, nex = gpm[g] >> 3, m = gpm[g] & 7u;
-    const uint32_t E = (uint32_t)q.x * 8u + 6u, cf = cols_of(q.y, q.z);
-    const bool cuttable = cf >= E && E <= v3::kSegMaxEnd;
-    uint32_t nseg = 1, last = x;
-    for (uint32_t w = fill_w0(C, x); w < C.nw; w++) {
-      if (fill_X(C, w) >= (uint64_t)x + c) break;
-      const uint32_t b = bnd[C.wb + w];
-      if (b > x && b < x + c && b != last) {
-        last = b;
-        const uint32_t J = b - x;
-        if (!cuttable || J + 64u > E || nseg > m) break;
-        cuts[(size_t)p * v3::kCutsPerPkt + nseg - 1] = (uint16_t)(J >> 8);
-        nseg++;
-      }
-    }
-    segs[p] = (uint8_t)nseg;
-    for (uint32_t k = 0; k <= m; k++)
-      if (8u * (nex + k) + j < (uint32_t)rows_cap)
-        items[8u * (nex + k) + j] = k < nseg ? make_int2(p, (int)(k | (nseg << 8))) : make_int2(-1, 0);
-  }
-  __syncthreads();
-  // waves no group starts (past a class's stream): empty, at the next class's first part
-  const uint32_t total = *rtotal;
-  const uint32_t cap = (uint32_t)max(rows_cap, 0) / 8u;
-  static_assert(kFillWavesMax <= 3 * 1024, "three waves a thread");
-  int32_t v[3];
-  for (int k = 0; k < 3; k++) {
-    const uint32_t w = (uint32_t)t + 1024u * k;
-    v[k] = w < NW ? wfirst[w] : 0;
-    if (w < NW && v[k] < 0) {
-      const int r = w < F[0].wb + F[0].nw ? 0 : w < F[1].wb + F[1].nw ? 1 : 2;
-      uint32_t e = total;
-      for (int r2 = r + 1; r2 < 3; r2++)
-        if (F[r2].nw) { e = (uint32_t)wfirst[F[r2].wb]; break; }   // (class starts are written)
-      v[k] = (int32_t)e;
-    }
-  }
-  __syncthreads();                                     // (every lane read the class starts above)
-  for (int k = 0; k < 3; k++) {
-    const uint32_t w = (uint32_t)t + 1024u * k;
-    if (w < NW) wfirst[w] = (int32_t)min((uint32_t)v[k], cap);
-  }
-  if (t == 0) {
-    wfirst[NW] = (int32_t)min(total, cap);
-    nrows[v3::kPlanRows] = (int32_t)(8u * NW);
-    nrows[v3::kPlanFixes] = 0;
-    nrows[v3::kPlanUniform] = 0;
-    nrows[v3::kPlanPacked] = 1;
-    nrows[v3::kPlanWave1] = (int32_t)F[1].wb;
-    nrows[v3::kPlanWave2] = (int32_t)F[2].wb;
-    nrows[v3::kPlanDropped] = 8u * total > (uint32_t)rows_cap ? (int32_t)(8u * total - (uint32_t)rows_cap) : 0;
-    nrows[v3::kPlanNcu] = max(ncu, 2);
-  }
-}
-
-// A mixed batch of the rx chain: the packed plan (its soft offsets are the chain's own, 256-B
-// aligned, and its stream columns fit 32 bits), else rows of whole frames and even segments.
-#ifndef ZRX_FILL_PLAN
-#define ZRX_FILL_PLAN 1
-#endif
-__device__ __forceinline__ void plan_mixed_rx(const int32_t* __restrict__ vparams, int npkts, uint64_t tcols, uint32_t L0,
-                                              int2* __restrict__ rows, int32_t* __restrict__ nrows,
-                                              uint8_t* __restrict__ segs, int32_t* __restrict__ order,
-                                              int32_t* __restrict__ out_bits, int ncu, int rows_cap, uint32_t* hist,
-                                              uint32_t* rtotal, int32_t* __restrict__ rfirst, uint16_t* __restrict__ cuts) {
-  // (from kFillMinPkts packets: a smaller batch does not fill the GPU either way)
-  if (ZRX_FILL_PLAN && rfirst && cuts && tcols < (1ull << 31) && npkts >= kFillMinPkts && npkts <= 8 * (kFillGroupsMax - 8)) {
-    plan_waves_fill(vparams, npkts, rows, nrows, segs, order, out_bits, ncu, rows_cap, hist, rtotal, rfirst, cuts);
-    return;
-  }
-  const uint32_t L = max(L0, v3::kMinSeg);
-  const uint32_t Lm = max(L * v3::kSegMixNum / 8u, v3::kMinSeg);
-  plan_rows_mixed(vparams, npkts, Lm, rows, nrows, segs, order, out_bits, ncu, rows_cap, hist, rtotal);
 }
 
 __global__ __launch_bounds__(1024) void k_pkt_plan(const int32_t* __restrict__ vparams, int npkts,
@@ -841,7 +527,6 @@ __global__ __launch_bounds__(1024) void k_pkt_plan(const int32_t* __restrict__ v
       nrows[v3::kPlanRows] = (int32_t)min((uint32_t)npkts * n0, (uint32_t)rows_cap);
       nrows[v3::kPlanFixes] = 0;
       nrows[v3::kPlanUniform] = (int32_t)n0;
-      nrows[v3::kPlanPacked] = 0;
       nrows[v3::kPlanDropped] = (uint32_t)npkts * n0 > (uint32_t)rows_cap ? (int32_t)((uint32_t)npkts * n0 - rows_cap) : 0;
       nrows[v3::kPlanNcu] = ncu;
       if (off) {                                       // the batch a next launch may reuse this plan for
@@ -899,8 +584,7 @@ __global__ __launch_bounds__(kPsThreads) void k_pkt_scan(const int32_t* __restri
                                                          int ncu, int rows_cap, int split,
                                                          int32_t* __restrict__ mixed_hint,
                                                          PlanScanRec* __restrict__ rec, uint32_t* __restrict__ ctr,
-                                                         uint32_t epoch, int32_t* __restrict__ rfirst,
-                                                         uint16_t* __restrict__ cuts) {
+                                                         uint32_t epoch) {
   constexpr int kW = kPsThreads / 64;
   __shared__ uint32_t wsum_u[kW], wsum_s[kW], wflag[kW];
   __shared__ unsigned long long wcols[kW];
@@ -1026,7 +710,9 @@ __global__ __launch_bounds__(kPsThreads) void k_pkt_scan(const int32_t* __restri
     for (int i = t; i < kOrderPerThread * 1024; i += kPsThreads) hist[i] = 0;
     if (t == 0) rtotal = 0;
     __syncthreads();
-    plan_mixed_rx(vparams, npkts, tcols, L0, rows, nrows, segs, order, out_bits, ncu, rows_cap, hist, &rtotal, rfirst, cuts);
+    const uint32_t L = max(L0, v3::kMinSeg);
+    const uint32_t Lm = max(L * v3::kSegMixNum / 8u, v3::kMinSeg);
+    plan_rows_mixed(vparams, npkts, Lm, rows, nrows, segs, order, out_bits, ncu, rows_cap, hist, &rtotal);
     return;
   }
   if (t != 0) return;
@@ -1037,7 +723,6 @@ __global__ __launch_bounds__(kPsThreads) void k_pkt_scan(const int32_t* __restri
   nrows[v3::kPlanRows] = (int32_t)min((uint32_t)npkts * n0, (uint32_t)rows_cap);
   nrows[v3::kPlanFixes] = 0;
   nrows[v3::kPlanUniform] = (int32_t)n0;
-  nrows[v3::kPlanPacked] = 0;
   nrows[v3::kPlanDropped] = (uint32_t)npkts * n0 > (uint32_t)rows_cap ? (int32_t)((uint32_t)npkts * n0 - rows_cap) : 0;
   nrows[v3::kPlanNcu] = ncu;
   nrows[v3::kPlanExpLen] = q0.x; nrows[v3::kPlanExpCr] = q0.y;
@@ -1055,8 +740,7 @@ __global__ __launch_bounds__(kPsThreads) void k_pkt_scan(const int32_t* __restri
 __global__ __launch_bounds__(1024) void k_pkt_rows(const int32_t* __restrict__ vparams, int npkts,
                                                    int2* __restrict__ rows, int32_t* __restrict__ nrows,
                                                    uint8_t* __restrict__ segs, int32_t* __restrict__ order,
-                                                   int32_t* __restrict__ out_bits, int ncu, int rows_cap,
-                                                   int32_t* __restrict__ rfirst, uint16_t* __restrict__ cuts) {
+                                                   int32_t* __restrict__ out_bits, int ncu, int rows_cap) {
   __shared__ uint32_t hist[kOrderPerThread * 1024];
   __shared__ uint32_t rtotal, uniform;
   __shared__ unsigned long long tcols;
@@ -1081,7 +765,9 @@ __global__ __launch_bounds__(1024) void k_pkt_rows(const int32_t* __restrict__ v
   if (uniform) return;
   const uint64_t rt = 64ull * (uint64_t)max(ncu, 1);   // (k_pkt_plan's segment length Lm)
   const uint32_t L0 = (uint32_t)min<uint64_t>((tcols + rt - 1) / rt, 0xFFFFFFFFull);
-  plan_mixed_rx(vparams, npkts, tcols, L0, rows, nrows, segs, order, out_bits, ncu, rows_cap, hist, &rtotal, rfirst, cuts);
+  const uint32_t L = max(L0, v3::kMinSeg);
+  const uint32_t Lm = max(L * v3::kSegMixNum / 8u, v3::kMinSeg);
+  plan_rows_mixed(vparams, npkts, Lm, rows, nrows, segs, order, out_bits, ncu, rows_cap, hist, &rtotal);
 }
 
 // ---- k_data_fft: FFT64 + GetData + DemapLimit + Demap + Deinterleave, lane = data symbol ----

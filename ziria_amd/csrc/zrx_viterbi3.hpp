@@ -477,7 +477,6 @@ __host__ __device__ __forceinline__ uint32_t rank_place(uint32_t r, uint32_t nfu
 // k_signal_vit raises when a packet of a batch of that size asks for something else: a
 // batch equal in all of it reuses the plan (k_pkt_plan returns at once).
 enum PlanWord { kPlanRows = 0, kPlanFixes = 1, kPlanUniform = 2, kPlanNcu = 3, kPlanSegLen = 4, kPlanDropped = 5,
-                kPlanPacked = 6, kPlanWave1 = 14, kPlanWave2 = 15,
                 kPlanExpN = 8, kPlanExpLen = 9, kPlanExpCr = 10, kPlanExpSoft = 11, kPlanExpMod = 12,
                 kPlanMismatch = 13, kPlanWords = 16 };
 constexpr int kPlanUnit = kRows;                       // rows ranked together by the mixed plan (a block's)
@@ -503,22 +502,6 @@ __host__ __device__ __forceinline__ uint32_t seg_stop(uint32_t E, uint32_t cols,
                                                       uint32_t warm = kSegWarm) {
   return k + 1u < nseg ? seg_start(E, nseg, k + 1u, warm) + warm + 30u : cols;
 }
-// Table geometry (a packed plan of a mixed batch, plan_waves_fill): the seams of packet p are
-// given, J_k = 256 cuts[p][k - 1] (k = 1 .. nseg - 1, increasing, J_k + 64 <= E), instead of
-// the formula's even cut.  Segment k starts at the body column S_k = 24 floor((J_k - 256) / 24),
-// so its warm-up J_k - S_k is 256..279 columns, and its seam column is C_k = S_k + 240 as with
-// the formula's W = 256.  The argument for exactness is the formula's: J_k is a window start
-// (a multiple of 256 columns from the frame's start) and S_k a body start.
-constexpr int kCutsPerPkt = kMaxSeg - 1;
-__host__ __device__ __forceinline__ uint32_t tab_start(uint32_t J) { return (J - 256u) / 24u * 24u; }
-__device__ __forceinline__ uint32_t seg_J(const uint16_t* __restrict__ cuts, bool tab, uint32_t p, uint32_t E,
-                                          uint32_t nseg, uint32_t k, uint32_t W) {
-  return tab ? 256u * (uint32_t)cuts[(size_t)p * kCutsPerPkt + k - 1u] : seg_start(E, nseg, k, W) + W;
-}
-__device__ __forceinline__ uint32_t seg_S(const uint16_t* __restrict__ cuts, bool tab, uint32_t p, uint32_t E,
-                                          uint32_t nseg, uint32_t k, uint32_t W) {
-  return tab ? tab_start(256u * (uint32_t)cuts[(size_t)p * kCutsPerPkt + k - 1u]) : seg_start(E, nseg, k, W);
-}
 // dump of seam j (1 <= j < nseg) of packet p, side 0 (segment j - 1) or 1 (segment j)
 __host__ __device__ __forceinline__ size_t seam_index(uint32_t p, uint32_t j, uint32_t side) {
   return (((size_t)p * (kMaxSeg - 1) + (j - 1u)) * 2u + side) * kSeamWords;
@@ -527,8 +510,8 @@ __host__ __device__ __forceinline__ size_t seam_index(uint32_t p, uint32_t j, ui
 // Cold per-row facts for the seam events, one entry per row of the block (LDS).
 struct RowX {
   uint32_t p;                                          // packet
-  uint32_t kn;                                         // k | nseg << 8 | fix << 16 | matched << 17 | short warm-up << 18 | table geometry << 19 | seam j << 20
-  uint32_t S, E;                                       // first column (absolute; packed rows: minus the row column it starts at), 8 len + 6
+  uint32_t kn;                                         // k | nseg << 8 | fix << 16 | matched << 17 | short warm-up << 18 | seam j << 20
+  uint32_t S, E;                                       // first column (absolute), 8 len + 6
 };
 
 // Per-row decoder state (row-uniform values in VGPRs).  Columns are relative to the row's
@@ -541,10 +524,6 @@ struct Row {
   uint32_t pT, plook, fT, fcnt, flook;
   uint32_t pM[kDw], fM[kDw];
   uint32_t nbytes;                    // bytes written so far
-  // packed rows (run_rows PACK): the row's next item and end in the item list, the row column
-  // its current item started at (its columns above are offset by it), an item not yet finished
-  uint32_t it, iend, t0;
-  bool cur;
 };
 
 __device__ __forceinline__ uint32_t row_next(const Row& R) {
@@ -582,10 +561,9 @@ __device__ __forceinline__ bool dump_ne(const uint2* __restrict__ a, const uint2
 // its metrics for the fix pass; a fix row compares its own with the next segment's start
 // state and, when they agree, stops where that segment's windows begin.
 __device__ __forceinline__ void seam_event(Row& R, uint32_t tr, const uint32_t (&M)[kDw], uint32_t l, uint32_t rib,
-                                        RowX* rowx, uint2* __restrict__ dumps, const uint16_t* __restrict__ cuts) {
+                                        RowX* rowx, uint2* __restrict__ dumps) {
   RowX x = rowx[rib];
   const uint32_t k = x.kn & 0xFFu, nseg = (x.kn >> 8) & 0xFFu, fix = (x.kn >> 16) & 1u, j = x.kn >> 20;
-  const bool tab = (x.kn >> 19) & 1u;
   const uint32_t W = (x.kn >> 18) & 1u ? kSegWarmUni : kSegWarm;
   (void)tr;
 #ifdef ZRX_GUARD
@@ -601,7 +579,7 @@ __device__ __forceinline__ void seam_event(Row& R, uint32_t tr, const uint32_t (
     dump_store(dumps + seam_index(x.p, j, side), l, M);
     if (side == 1u && k + 1u < nseg) {
       x.kn = (x.kn & 0xFFFFFu) | ((k + 1u) << 20);
-      R.evc = seg_S(cuts, tab, x.p, x.E, nseg, k + 1u, W) + seg_cmp(W) - x.S;
+      R.evc = seg_start(x.E, nseg, k + 1u, W) + seg_cmp(W) - x.S;
     } else {
       R.evc = kNever;
     }
@@ -613,12 +591,12 @@ __device__ __forceinline__ void seam_event(Row& R, uint32_t tr, const uint32_t (
     for (int i = 0; i < kDw; i++) d |= M[i] ^ B[i];
     const uint64_t bad = __builtin_amdgcn_ballot_w64((d & 0x7F007F00u) != 0u);
     if (row_bits(bad) == 0u) {                         // the row's 64 H bytes agree
-      R.cols = min(R.cols, seg_J(cuts, tab, x.p, x.E, nseg, j, W) + 30u - x.S);
+      R.cols = min(R.cols, seg_start(x.E, nseg, j, W) + W + 30u - x.S);
       x.kn |= 1u << 17;
       R.evc = kNever;
     } else if (j + 1u < nseg) {
       x.kn = (x.kn & 0xFFFFFu) | ((j + 1u) << 20);
-      R.evc = seg_S(cuts, tab, x.p, x.E, nseg, j + 1u, W) + seg_cmp(W) - x.S;
+      R.evc = seg_start(x.E, nseg, j + 1u, W) + seg_cmp(W) - x.S;
     } else {
       R.evc = kNever;
     }
@@ -655,8 +633,7 @@ __device__ __forceinline__ void events(Row& R, uint32_t tr, const uint32_t (&M)[
 // byte read before into a dword, moves the ring index on and issues the next read; every
 // fourth output byte stores the dword with a buffer store (rows that do not own the window
 // store out of range, i.e. nothing).  The slot base steps back on the scalar unit.
-// we = nl (0: nothing deferred).  (A frame's final window deferred the same way, byte stores
-// and all, measured slower than walking it at once: PERFLOG round 6.)
+// we = nl (0: nothing deferred).
 struct Walk {
   int we;                         // wave-uniform
   uint32_t A;                     // wave-uniform: slot of the pending read
@@ -815,9 +792,7 @@ __device__ __forceinline__ void traceback(bool due, const uint32_t (&M)[kDw], ui
   // six columns; those windows walk now).
   const uint32_t s = (tr0 + 22u - C0f) >> 3;
   const uint32_t nlf = (C0f - chf) >> 3;
-  // output byte of block c_hi, newest first (a 32-bit sum: a packed row's ooff is offset by
-  // -t0 / 8 and may wrap)
-  uint8_t* op = out + (uint32_t)(ooff + ((c_hi - 14u) >> 3));
+  uint8_t* op = out + ooff + ((c_hi - 14u) >> 3);      // output byte of block c_hi, newest first
   auto prevS = [](uint32_t x) { return x == 0u ? span - (uint32_t)kSlotBytes : x - (uint32_t)kSlotBytes; };
 #ifdef ZRX_GUARD
   if (walker && ZG_OUT_BAD(op + 1 - (int)nout, op + 1)) {
@@ -930,7 +905,6 @@ struct Packet {
   Walk* W;                                             // deferred traceback tail (WS >= 0 bodies)
   RowX* rowx;                                          // the block's cold row facts (seam events)
   uint2* dumps;                                        // seam dumps
-  const uint16_t* cuts;                                // table geometry (packed plans)
 
   // P word of body column J: lane J mod kLanes of the row built it as its word J / kLanes
   template <int J>
@@ -1029,7 +1003,7 @@ static __device__ __forceinline__ void ds_b8_hi(uint32_t a, uint32_t v) {
         if (tr >= s_next) {
           // seam events sit on body ends (seam columns are multiples of 24 from the row's start)
           if constexpr (c == 24)
-            if (R.live && tr == R.evc) seam_event(R, tr, M, l, rib, rowx, dumps, cuts);
+            if (R.live && tr == R.evc) seam_event(R, tr, M, l, rib, rowx, dumps);
           events(R, tr, M);
           s_next = wave_min_rows(R.next);
         }
@@ -1122,80 +1096,10 @@ __device__ __forceinline__ uint32_t row16_max(uint32_t x) {
   x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x121, 0xF, 0xF, false));   // row_ror:1
   return x;
 }
-// A packed plan's rows (plan_waves_fill): wave w decodes parts wfirst[w] .. wfirst[w + 1] - 1 one
-// after another, its row j taking item 8 i + j of part i, item = {packet, k | nseg << 8} (segment
-// k of nseg, table geometry) or {-1, 0} (nothing); a wave's items share a rate.  The 8 rows
-// start a part together, when none of them is live any more, at a body start t0 of the wave (a
-// multiple of 24, so every column phase is the frame's own, and the rows' windows fall on the
-// same columns): an item's row fields are offset by t0, its output offset by -t0 / 8 and its
-// soft fetch offset by the fetch base at t0, and it starts from ALL_INIT0 (k = 0) or zero
-// metrics (k > 0).
-struct PackCtx {
-  const int2* __restrict__ items;
-  const int32_t* __restrict__ rfirst;                  // a wave's first part
-  uint32_t wave1, wave2;                               // the first waves of rates 1 and 2
-  const int32_t* __restrict__ vparams;
-  const int64_t* __restrict__ soft_off;
-  const int64_t* __restrict__ out_off;
-  int32_t* __restrict__ out_bits;
-  const uint16_t* __restrict__ cuts;
-};
-// The next item of a row that needs one: row fields, cold facts, metrics, fetch offset, output
-// offset.  (Rows of a rate other than the pass's never occur: the plan keeps rates apart.)
-template <int CR>
-__device__ __forceinline__ void pack_setup(Row& R, uint32_t (&M)[kDw], uint32_t t0, uint32_t l, uint32_t rib, RowX* rowx,
-                                           const PackCtx& P, int64_t lo_w, uint32_t base, uint32_t off0,
-                                           uint32_t& vo0, uint32_t& ooff) {
-  const int2 e = P.items[R.it];
-  R.it += 8;
-  if (e.x < 0) {                                       // nothing for this row in the part
-    R.live = false; R.cur = false; R.next = kNever;
-    return;
-  }
-  const uint32_t p = (uint32_t)e.x, k = (uint32_t)e.y & 0xFFu, nseg = ((uint32_t)e.y >> 8) & 0xFFu;
-  const int4 q = *reinterpret_cast<const int4*>(P.vparams + 4 * (int64_t)p);   // {frame_len, cr, soft_len, mod}
-  const uint32_t u = (uint32_t)max(q.z, 0);
-  const uint32_t cols = q.y != CR ? 0u : CR == 0 ? u >> 1 : CR == 1 ? (u / 3u) * 2u : (u >> 2) * 3u;
-  const uint32_t E = (uint32_t)q.x * 8u + 6u;
-  const uint32_t S = k ? seg_S(P.cuts, true, p, E, nseg, k, kSegWarm) : 0u;
-  const uint32_t stop = k + 1u < nseg ? seg_J(P.cuts, true, p, E, nseg, k + 1u, kSegWarm) + 30u : cols;
-  const uint32_t j = k ? k : 1u;
-  rowx[rib] = RowX{p, k | (nseg << 8) | (1u << 19) | (j << 20), S - t0, E};
-  constexpr uint32_t st = Rate<CR>::steps, G = Rate<CR>::G;
-  const uint32_t sS = S / st * G;                      // soft values before S (S is a body start)
-  R.t0 = t0;
-  R.ob = t0 + (k ? seg_J(P.cuts, true, p, E, nseg, k, kSegWarm) - S : 0u);
-  R.end = t0 + E - S;
-  R.cols = t0 + (cols > S ? min(cols, stop) - S : 0u);
-  R.evc = j < nseg ? t0 + seg_S(P.cuts, true, p, E, nseg, j, kSegWarm) + seg_cmp(kSegWarm) - S : kNever;
-  R.live = cols > S;
-  R.cur = true;
-  R.ppend = R.fpend = false;
-  R.nbytes = 0;
-  R.next = row_next(R);
-#pragma unroll
-  for (int d = 0; d < kDw; d++)
-    M[d] = k ? 0u : ((pos_of(l, d, 1) ? 24u : 0u) << 24) | ((pos_of(l, d, 0) ? 24u : 0u) << 8);   // ALL_INIT0
-  // (soft offsets are 256-B units in the rx chain and sS a multiple of 4: the lane's byte
-  // phase within its dwords stays the one run_rows set up)
-  vo0 = (uint32_t)(P.soft_off[p] + (int64_t)sS - lo_w) + (off0 & ~3u) - base;
-  ooff = (uint32_t)(P.out_off[p] + (int64_t)(S >> 3)) - (t0 >> 3);   // (out_off: from out, within 4 GiB)
-}
-// A finished item: the frame's bit count from its last segment (viterbi_rows' rule).
-__device__ __forceinline__ void pack_finish(Row& R, uint32_t l, uint32_t rib, const RowX* rowx, const PackCtx& P) {
-  R.cur = false;
-  const RowX x = rowx[rib];
-  if (l == 0 && (x.kn & 0xFFu) + 1u == ((x.kn >> 8) & 0xFFu)) {
-    const uint32_t S = x.S + R.t0;
-    P.out_bits[x.p] = R.nbytes == 0xFFFFFFFFu ? -1
-                      : (int32_t)(((R.nbytes ? R.nbytes - (R.t0 >> 3) : 0u) + (S >> 3)) * 8u);
-  }
-}
-template <int CR, int DBG, bool PACK = false>
+template <int CR, int DBG>
 __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64_t so, uint32_t n, Row& R, const Consts& K, uint32_t l,
                          uint32_t rib, uint8_t* ring_block, uint8_t* __restrict__ out, uint32_t ooff,
-                         uint32_t (&M)[kDw], RowX* rowx, uint2* __restrict__ dumps, bool prio, bool younger,
-                         const uint16_t* __restrict__ cuts = nullptr, const PackCtx* PC = nullptr) {
+                         uint32_t (&M)[kDw], RowX* rowx, uint2* __restrict__ dumps, bool prio, bool younger) {
   using RT = Rate<CR>;
   // guard ANDs outside the speculative bodies: rate 3/4 only (Guard-free columns)
   constexpr bool kG = CR == 2 || !kNoGuard;
@@ -1205,7 +1109,7 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
   W.ix = W.b = W.acc = 0;
   W.voff = 0x80000000u;
   W.ob = (uint64_t)(uintptr_t)out;
-  Packet<CR, DBG> pk{K, R, l, rib, ring_block, ring_block, &W, rowx, dumps, cuts};
+  Packet<CR, DBG> pk{K, R, l, rib, ring_block, ring_block, &W, rowx, dumps};
   // this lane builds the P words of body columns kLanes i + l (i < kPw; 16-lane rows: the
   // second word of lanes 8..15 repeats lanes 0..7's)
   // Soft values by buffer loads: one wave-uniform descriptor over the rows' soft windows,
@@ -1214,26 +1118,10 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
   // the descriptor and return 0; reads past a row's own end read its neighbour's values,
   // which feed only columns beyond R.cols.  The caller (k_viterbi3) passes rows whose soft
   // values lie within kSoftWindow of each other.
-  int64_t lo_me = R.live ? so : INT64_MAX, hi_me = R.live ? so + (int64_t)n : INT64_MIN;
-  if constexpr (PACK) {                                // the window over every item of the wave's rows
-    for (uint32_t i = R.it; i < R.iend; i += 8) {
-      const int32_t pi = PC->items[i].x;
-      if (pi < 0) continue;
-      const uint32_t p = (uint32_t)pi;
-      const int64_t o = PC->soft_off[p];
-      lo_me = min(lo_me, o);
-      hi_me = max(hi_me, o + (int64_t)max(PC->vparams[4 * (int64_t)p + 2], 0));
-    }
-  }
+  const int64_t lo_me = R.live ? so : INT64_MAX, hi_me = R.live ? so + (int64_t)n : INT64_MIN;
   const int64_t lo_w = wave_min_rows64(lo_me) & ~(int64_t)3;   // (dword-aligned: soft is)
   const int64_t hi_w = (wave_max_rows64(hi_me) + 3) & ~(int64_t)3;
   if (hi_w - lo_w > kSoftWindow) {                     // one row's soft values beyond 4 GiB: not decodable
-    if constexpr (PACK) {
-      for (; R.it < R.iend; R.it += 8) {               // (never in the rx chain: its soft values are packed)
-        const int2 e = PC->items[R.it];
-        if (l == 0 && e.x >= 0 && (e.y & 0xFF) + 1 == ((e.y >> 8) & 0xFF)) PC->out_bits[e.x] = -1;
-      }
-    }
     if (R.live) R.nbytes = 0xFFFFFFFFu;
     return;
   }
@@ -1246,9 +1134,8 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
   // every 6 columns, so k is a constant)
   constexpr int nD = !kDwFetch ? 2 * kPw : kLanes == 8 ? (CR == 0 ? 3 : 2) : (CR == 2 ? 3 : 4);
   uint32_t vo[kDwFetch ? 1 : kPw], selA[kPw], selB[kPw];
-  const uint32_t off0 = soft_off<CR>((uint32_t)kCpl * l);   // (kDwFetch) the lane's first byte in a body chunk
   if constexpr (kDwFetch) {
-    const uint32_t j0 = (uint32_t)kCpl * l;
+    const uint32_t j0 = (uint32_t)kCpl * l, off0 = soft_off<CR>(j0);
     const uint32_t w0 = rel + off0, sh = w0 & 3u;
     vo[0] = w0 & ~3u;
 #pragma unroll
@@ -1274,14 +1161,6 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
   // soft words / bytes of the next kPf bodies in flight (sd[0]: the next body's)
   uint32_t sd[kPf][nD];
   auto fetch_into = [&](uint32_t (&D)[nD], uint32_t base) {
-    if constexpr (PACK) {                              // one descriptor; the rows' offsets move
-      static_assert(!PACK || kDwFetch, "packed rows fetch dwords");
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(soft + lo_w), (short)0, (int)(uint32_t)(hi_w - lo_w), 0x00020000);
-#pragma unroll
-      for (int d = 0; d < nD; d++) D[d] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(vo[0] + base) + 4 * d, 0, 0);
-      return;
-    }
     const int64_t left = hi_w - lo_w - (int64_t)base;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(soft + lo_w + base), (short)0, (int)(uint32_t)(left > 0 ? left : 0), 0x00020000);
@@ -1373,23 +1252,7 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
       }
     }
   };
-  // Packed rows: when no row of the wave is live any more (their tracebacks ran in the bodies
-  // of the last pass), the rows take their items of the next part at this body start.
-  auto pack_refill = [&]() {
-    if constexpr (PACK) {
-      if (R.cur && !R.live) pack_finish(R, l, rib, rowx, *PC);
-      if (__builtin_amdgcn_ballot_w64(R.live) != 0) return;
-      const bool need = R.it < R.iend;
-      if (__builtin_amdgcn_ballot_w64(need) == 0) return;
-      if (W.we) walk_finish(W, ring_block, rib * 64u);   // (its reads come before the new items' snapshots)
-      if (need) pack_setup<CR>(R, M, tr0, l, rib, rowx, *PC, lo_w, base, off0, vo[0], ooff);
-#pragma unroll
-      for (int q = 0; q < kPf; q++) fetch_into(sd[q], base + q * RT::chunk);
-      s_next = wave_min_rows(R.next);
-    }
-  };
-  while (__builtin_amdgcn_ballot_w64(R.live || (PACK && R.it < R.iend)) != 0) {
-    pack_refill();
+  while (__builtin_amdgcn_ballot_w64(R.live) != 0) {
     // The hot loop: bodies with no event due, no deferred walk, nothing else on this path
     // (its own loop, so the register allocator keeps the loop-carried values in place).
     while ((DBG & 16) || (s_next > tr0 + 24 && s_next != kNever)) {
@@ -1417,10 +1280,7 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
       }
     }
     if constexpr ((DBG & 16) != 0) break;
-    if (s_next == kNever) {                            // every row is done (packed: with its item)
-      if constexpr (PACK) continue;
-      break;
-    }
+    if (s_next == kNever) break;                       // every row is done
     // A body with an event due: checked, then the tracebacks it raised.
     {
       uint32_t Pw[kPw];
@@ -1451,12 +1311,11 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
       walk_uniform(W);
       R.ppend = false;
     }
-    if ((DBG & 4097) == 0 && __builtin_amdgcn_ballot_w64(R.fpend) != 0) {
+    if ((DBG & 1) == 0 && __builtin_amdgcn_ballot_w64(R.fpend) != 0) {
       traceback(R.fpend, R.fM, R.fT, R.fcnt, R.flook, l, rib, ring_block, out, ooff, R.nbytes);
       R.fpend = false;
     }
     if constexpr ((DBG & 1) != 0) R.ppend = R.fpend = false;
-    if constexpr ((DBG & 4096) != 0) R.fpend = false;   // (timing: no final tracebacks)
     next_body();
     // A deferred traceback walk runs in the next body's columns.
     if (W.we && __builtin_amdgcn_ballot_w64(R.live) != 0) {
@@ -1507,18 +1366,11 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
         else pk.template body<true, 2, kG, false>(M, Pw, tr0, s_next, cols24);
       }
       W.we = 0;
-      // windows that came due in this body walk now: the ring keeps a window's snapshots for
-      // one more body only (rows with unaligned windows, e.g. packed rows, meet these)
-      if ((DBG & 1) == 0 && __builtin_amdgcn_ballot_w64(R.ppend) != 0) {
-        traceback(R.ppend, R.pM, R.pT, 256u, R.plook, l, rib, ring_block, out, ooff, R.nbytes);
-        R.ppend = false;
-      }
-      if ((DBG & 4097) == 0 && __builtin_amdgcn_ballot_w64(R.fpend) != 0) {
+      if ((DBG & 1) == 0 && __builtin_amdgcn_ballot_w64(R.fpend) != 0) {   // (a partial window is 256 columns on)
         traceback(R.fpend, R.fM, R.fT, R.fcnt, R.flook, l, rib, ring_block, out, ooff, R.nbytes);
         R.fpend = false;
       }
       if constexpr ((DBG & 1) != 0) R.ppend = R.fpend = false;
-    if constexpr ((DBG & 4096) != 0) R.fpend = false;   // (timing: no final tracebacks)
       next_body();
     }
   }
@@ -1529,9 +1381,6 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
     }
   }
   if (W.we) walk_finish(W, ring_block, rib * 64u);     // rows done before the deferred tail ran
-  if constexpr (PACK) {
-    if (R.cur) pack_finish(R, l, rib, rowx, *PC);
-  }
 }
 
 }  // namespace v3
@@ -1558,8 +1407,7 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
                                              const int32_t* __restrict__ vparams, uint8_t* __restrict__ out,
                                              const int64_t* __restrict__ out_off, int32_t* __restrict__ out_bits,
                                              const int2* __restrict__ rows, const uint8_t* __restrict__ segs,
-                                             uint2* __restrict__ dumps, int32_t* __restrict__ stats,
-                                             const uint16_t* __restrict__ cuts, bool tab) {
+                                             uint2* __restrict__ dumps, int32_t* __restrict__ stats) {
   constexpr int fix = FIX;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t l = lane & (v3::kLanes - 1u);
@@ -1618,22 +1466,17 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
       // from segment ks - 1's state and may stop only at a later seam past kl whose start
       // state it reproduces (every segment after that one then starts right).
       uint32_t ks = 0, kl = 0;
-      // every seam's two dumps loaded at once (a seam past the row's reads seam 1 and is
-      // ignored), then compared: one round of load latency instead of one per seam
-      if (__builtin_amdgcn_ballot_w64(work && nseg > 1u) != 0) {
-#pragma unroll
-        for (uint32_t jj = 1; jj < (uint32_t)v3::kMaxSeg; jj++) {
-          const bool in = work && jj < nseg;
-          const uint32_t js = in ? jj : 1u;
-          const bool ne = v3::dump_ne(dumps + v3::seam_index((uint32_t)p, js, 0), dumps + v3::seam_index((uint32_t)p, js, 1), l) && in;
-          if (v3::row_bits(__builtin_amdgcn_ballot_w64(ne)) != 0u) {
-            if (ks == 0u) ks = jj;
-            kl = jj;
-          }
+      for (uint32_t jj = 1; __builtin_amdgcn_ballot_w64(work && jj < nseg) != 0; jj++) {
+        const bool ne = work && jj < nseg &&
+                        v3::dump_ne(dumps + v3::seam_index((uint32_t)p, jj, 0), dumps + v3::seam_index((uint32_t)p, jj, 1), l);
+        const uint64_t bad = __builtin_amdgcn_ballot_w64(ne);
+        if (v3::row_bits(bad) != 0u) {
+          if (ks == 0u) ks = jj;
+          kl = jj;
         }
       }
       work = work && ks != 0u;
-      if (work) { S = v3::seg_S(cuts, tab, (uint32_t)p, E, nseg, ks, W) + v3::seg_cmp(W); j = kl + 1u; k = ks; }
+      if (work) { S = v3::seg_start(E, nseg, ks, W) + v3::seg_cmp(W); j = kl + 1u; k = ks; }
 #ifdef ZRX_GUARD
       if (work && l == 0)
         printf("ZG fix row: blk %d rib %u p %d nseg %u ks %u S %u E %u cols %u cr %d n %d\n", (int)blockIdx.x, rib, p, nseg,
@@ -1647,8 +1490,7 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
     }
     // (cold facts in LDS: read back where needed instead of held in registers by the decode)
     // (fix rows: k holds ks, the seam they start at)
-    rowx[rib] = v3::RowX{(uint32_t)p, k | (nseg << 8) | ((uint32_t)(fix != 0) << 16) | ((uint32_t)(uni != 0u) << 18) |
-                                          ((uint32_t)tab << 19) | (j << 20),
+    rowx[rib] = v3::RowX{(uint32_t)p, k | (nseg << 8) | ((uint32_t)(fix != 0) << 16) | ((uint32_t)(uni != 0u) << 18) | (j << 20),
                          S, E};
     const int64_t sS = work ? (int64_t)(S / (uint32_t)(cr + 1)) * (cr == 0 ? 2 : cr == 1 ? 3 : 4) : 0;   // soft values before S
     so += sS;
@@ -1699,14 +1541,9 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
         if (younger) __builtin_amdgcn_s_sleep(ZRX_STAGGER);   // (experiment: offset the SIMD's two waves)
 #endif
         v3::Row Rr;
-        // (the first window: J_k, k the segment or the fix row's first seam; J_k - S_k = W
-        // with the formula)
-        const uint32_t xJ = xk ? v3::seg_J(cuts, tab, x.p, x.E, xn, xk, xw) : 0u;
-        const uint32_t xS = xk ? v3::seg_S(cuts, tab, x.p, x.E, xn, xk, xw) : 0u;
-        Rr.ob = xfix ? xJ - (xS + v3::seg_cmp(xw)) : xk ? xJ - xS : 0u;
+        Rr.ob = xfix ? xw - v3::seg_cmp(xw) : xk ? xw : 0u;
         Rr.end = x.E - x.S; Rr.cols = colsS;
-        Rr.evc = xj != 0u && xj < xn ? v3::seg_S(cuts, tab, x.p, x.E, xn, xj, xw) + v3::seg_cmp(xw) - x.S : v3::kNever;
-        Rr.it = Rr.iend = Rr.t0 = 0; Rr.cur = false;
+        Rr.evc = xj != 0u && xj < xn ? v3::seg_start(x.E, xn, xj, xw) + v3::seg_cmp(xw) - x.S : v3::kNever;
         Rr.live = mq;
         Rr.ppend = Rr.fpend = false;
         Rr.pT = Rr.plook = Rr.fT = Rr.fcnt = Rr.flook = 0;
@@ -1714,9 +1551,9 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
         for (int d = 0; d < v3::kDw; d++) Rr.pM[d] = Rr.fM[d] = 0u;
         Rr.nbytes = 0;
         Rr.next = v3::row_next(Rr);
-        if (rate == 0) v3::run_rows<0, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M, rowx, dumps, lrpt, younger, cuts);
-        else if (rate == 1) v3::run_rows<1, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M, rowx, dumps, lrpt, younger, cuts);
-        else v3::run_rows<2, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M, rowx, dumps, lrpt, younger, cuts);
+        if (rate == 0) v3::run_rows<0, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M, rowx, dumps, lrpt, younger);
+        else if (rate == 1) v3::run_rows<1, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M, rowx, dumps, lrpt, younger);
+        else v3::run_rows<2, DBG>(soft, so, nS, Rr, K, l, rib, ring, obase, ooff, M, rowx, dumps, lrpt, younger);
         if (mq) nbytes = Rr.nbytes;
       }
     }
@@ -1739,48 +1576,13 @@ __device__ __forceinline__ void viterbi_rows(int g0, int nrows, uint32_t uni, ui
 #endif
   }
 }
-// The rows of a packed plan (v3::PackCtx): every row slot decodes its items in turn; the rows
-// of a wave share a rate (one run_rows pass).
-template <int DBG>
-__device__ __forceinline__ void viterbi_rows_packed(int g0, int nrows, uint32_t ncu, const v3::Consts& K, uint8_t* ring,
-                                                    v3::RowX* rowx, const uint8_t* __restrict__ soft, uint8_t* __restrict__ out,
-                                                    uint2* __restrict__ dumps, const v3::PackCtx& P) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t l = lane & (v3::kLanes - 1u);
-  const uint32_t rib = threadIdx.x >> v3::kLaneBits;
-  const int slot = g0 + (int)rib;
-  const bool valid = slot < nrows;
-  // (a wave's rows: slots 8w .. 8w + 7.  Placing a CU's 8 waves on consecutive waves of the
-  // plan, so that they share a rate and its code, measured the same: PERFLOG round 6.)
-  const uint32_t w = (uint32_t)slot >> 3, j = (uint32_t)slot & 7u;
-  const uint32_t i0 = valid ? 8u * (uint32_t)P.rfirst[w] + j : 0u, i1 = valid ? 8u * (uint32_t)P.rfirst[w + 1] + j : 0u;
-  const int cr = !valid ? -1 : w < P.wave1 ? 0 : w < P.wave2 ? 1 : 2;   // (the waves of a rate are consecutive)
-  const bool younger = v3::kPrioMode != 2 && ((blockIdx.x / ncu) & 1u) != 0u;
-  for (int rate = 0; rate < 3; rate++) {
-    const bool mine = cr == rate;
-    if (__builtin_amdgcn_ballot_w64(mine) == 0) continue;
-    v3::Row Rr;
-    Rr.it = mine ? i0 : 0u; Rr.iend = mine ? i1 : 0u; Rr.t0 = 0; Rr.cur = false;
-    Rr.live = false; Rr.ppend = Rr.fpend = false;
-    Rr.ob = Rr.end = Rr.cols = 0; Rr.evc = v3::kNever; Rr.next = v3::kNever; Rr.nbytes = 0;
-    Rr.pT = Rr.plook = Rr.fT = Rr.fcnt = Rr.flook = 0;
-    uint32_t M[v3::kDw];
-#pragma unroll
-    for (int d = 0; d < v3::kDw; d++) Rr.pM[d] = Rr.fM[d] = M[d] = 0u;
-    if (rate == 0) v3::run_rows<0, DBG, true>(soft, 0, 0, Rr, K, l, rib, ring, out, 0, M, rowx, dumps, false, younger, P.cuts, &P);
-    else if (rate == 1) v3::run_rows<1, DBG, true>(soft, 0, 0, Rr, K, l, rib, ring, out, 0, M, rowx, dumps, false, younger, P.cuts, &P);
-    else v3::run_rows<2, DBG, true>(soft, 0, 0, Rr, K, l, rib, ring, out, 0, M, rowx, dumps, false, younger, P.cuts, &P);
-  }
-}
-// rfirst, cuts: a packed plan's row starts and seam table (the plan header says which plan).
 template <int DBG, bool FIX = false>
 __global__ __launch_bounds__(256, v3::kWavesPerSimd) void k_viterbi3(const uint8_t* __restrict__ soft, const int64_t* __restrict__ soft_off,
                                                   const int32_t* __restrict__ vparams, int nslots,
                                                   uint8_t* __restrict__ out, const int64_t* __restrict__ out_off,
                                                   int32_t* __restrict__ out_bits, const int2* __restrict__ rows,
                                                   int32_t* __restrict__ nrows_p, const uint8_t* __restrict__ segs,
-                                                  uint2* __restrict__ dumps, const int32_t* __restrict__ rfirst = nullptr,
-                                                  const uint16_t* __restrict__ cuts = nullptr) {
+                                                  uint2* __restrict__ dumps) {
   __shared__ uint8_t ring[v3::kRing * v3::kSlotBytes];
   __shared__ v3::RowX rowx[v3::kRows];
   // the plan header (v3::PlanWord): rows, the fix pass's count of re-decoded rows, the
@@ -1789,26 +1591,18 @@ __global__ __launch_bounds__(256, v3::kWavesPerSimd) void k_viterbi3(const uint8
   const uint32_t uni = nrows_p ? (uint32_t)nrows_p[v3::kPlanUniform] : 0u;
   const uint32_t ncu = nrows_p ? max((uint32_t)nrows_p[v3::kPlanNcu], 2u) : 2u;
   const uint32_t ncu_rcp = 0xFFFFFFFFu / ncu + 1u;
-  const bool packed = nrows_p && nrows_p[v3::kPlanPacked] != 0 && rfirst && cuts;
   if (FIX && uni == 1u) return;                        // a uniform batch of whole frames has no seams
   v3::Consts K;
   v3::make_consts(K, threadIdx.x & (v3::kLanes - 1u), threadIdx.x >> v3::kLaneBits);
   if constexpr (FIX) {                                 // block-stride over the packets
     for (int g0 = blockIdx.x * v3::kRows; g0 < nrows; g0 += gridDim.x * v3::kRows)
       viterbi_rows<DBG, true>(g0, nrows, uni, ncu, ncu_rcp, K, ring, rowx, soft, soft_off, vparams, out, out_off, out_bits, rows, segs, dumps,
-                              nrows_p, cuts, packed);
+                              nrows_p);
   } else {
     const int g0 = blockIdx.x * v3::kRows;
-    if (g0 < nrows) {
-      if (packed) {
-        const v3::PackCtx P{rows, rfirst, (uint32_t)nrows_p[v3::kPlanWave1], (uint32_t)nrows_p[v3::kPlanWave2], vparams, soft_off,
-                            out_off, out_bits, cuts};
-        viterbi_rows_packed<DBG>(g0, nrows, ncu, K, ring, rowx, soft, out, dumps, P);
-      } else {
-        viterbi_rows<DBG, false>(g0, nrows, uni, ncu, ncu_rcp, K, ring, rowx, soft, soft_off, vparams, out, out_off, out_bits, rows, segs,
-                                 dumps, nullptr, nullptr, false);
-      }
-    }
+    if (g0 < nrows)
+      viterbi_rows<DBG, false>(g0, nrows, uni, ncu, ncu_rcp, K, ring, rowx, soft, soft_off, vparams, out, out_off, out_bits, rows, segs,
+                               dumps, nullptr);
   }
 }
 

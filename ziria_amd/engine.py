@@ -63,23 +63,6 @@ class RxEngine:
         check(lib().zrx_plan_stats(self._h, st), "zrx_plan_stats")
         return int(st[0]), int(st[1])
 
-    def plan_dump(self, npkts):
-        """The last plan (zrx_plan_dump): header words, and for a packed plan the item list
-        [n, 2] (8 a part), the waves' first parts [waves + 1], segments per packet and the seam
-        table [npkts, 7]."""
-        import numpy as np
-        hdr = np.zeros(16, np.int32)
-        cap_rows = 2056
-        cap_items = int(npkts) + 8 * cap_rows + 64
-        items = np.zeros((cap_items, 2), np.int32)
-        rfirst = np.zeros(cap_rows + 1, np.int32)
-        segs = np.zeros(int(npkts), np.uint8)
-        cuts = np.zeros((int(npkts), 7), np.uint16)
-        ptr = lambda a: a.ctypes.data_as(C.c_void_p)
-        check(lib().zrx_plan_dump(self._h, ptr(hdr), ptr(items), cap_items, ptr(rfirst), cap_rows, ptr(segs), ptr(cuts),
-                                  int(npkts)), "zrx_plan_dump")
-        return dict(header=hdr, items=items, wfirst=rfirst, segs=segs, cuts=cuts)
-
     def plan_check(self):
         """Raises if the last Viterbi plan dropped rows past its workspace bound (ZRX_EPLAN)."""
         check(lib().zrx_plan_check(self._h), "zrx_plan_check")
