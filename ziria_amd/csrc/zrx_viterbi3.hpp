@@ -1002,8 +1002,10 @@ static __device__ __forceinline__ void ds_b8_hi(uint32_t a, uint32_t v) {
         const uint32_t tr = tr0 + c;
         if (tr >= s_next) {
           // seam events sit on body ends (seam columns are multiples of 24 from the row's start)
+          // (a speculative body runs it only once its checks passed, so a redo never has to
+          // restore the row's cold facts)
           if constexpr (c == 24)
-            if (R.live && tr == R.evc) seam_event(R, tr, M, l, rib, rowx, dumps);
+            if (R.live && tr == R.evc && (!CHK || ok)) seam_event(R, tr, M, l, rib, rowx, dumps);
           events(R, tr, M);
           s_next = wave_min_rows(R.next);
         }
@@ -1292,13 +1294,11 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
 #pragma unroll
         for (int d = 0; d < kDw; d++) M0[d] = M[d];
         const Row R0 = R;
-        const RowX x0 = rowx[rib];
         const uint32_t s0 = s_next;
         if (!pk.template body<true, 0, false, true>(M, Pw, tr0, s_next, cols24, __builtin_amdgcn_ballot_w64(!R.live))) {
 #pragma unroll
           for (int d = 0; d < kDw; d++) M[d] = M0[d];
           R = R0;
-          rowx[rib] = x0;
           s_next = s0;
           pk.template body<true, 0, true, false>(M, Pw, tr0, s_next, cols24);
         }
@@ -1344,7 +1344,6 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
           }
         } else {
           const Row R0 = R;
-          const RowX x0 = rowx[rib];
           const uint32_t s0 = s_next;
           const uint64_t dead = __builtin_amdgcn_ballot_w64(!R.live);
           const bool ok = W.we == 3 ? pk.template body<true, 3, false, true>(M, Pw, tr0, s_next, cols24, dead)
@@ -1353,7 +1352,6 @@ __device__ __forceinline__ void run_rows(const uint8_t* __restrict__ soft, int64
 #pragma unroll
             for (int d = 0; d < kDw; d++) M[d] = M0[d];
             R = R0;
-            rowx[rib] = x0;
             s_next = s0;
             pk.template body<true, 0, true, false>(M, Pw, tr0, s_next, cols24);
           }
