@@ -188,6 +188,24 @@ __device__ __forceinline__ void demap_deinterleave_st(const s2* x, Lut lut, St s
   }
   soft_units<MOD>(lr, li, st, std::make_integer_sequence<int, NC / 16>{});
 }
+// The same in two steps, so that a wave whose lanes mix modulations reads the LUT once: the
+// LUT words of both components of the 48 data bins (a BPSK lane's li go unused: the LUT
+// index is the clipped component whatever the modulation), then the packing of MOD.
+template <class Lut>
+__device__ __forceinline__ void demap_lut_words(const s2* x, Lut lut, uint32_t (&lr)[48], uint32_t (&li)[48]) {
+#pragma unroll
+  for (int i = 0; i < 48; i++) {
+    s2 v = x[bitrev6(data_bin(i))];
+    v = __builtin_elementwise_max(__builtin_elementwise_min(v, (s2){127, 127}), (s2){-128, -128});
+    const uint32_t u = as_u32(v);
+    lr[i] = lut(u & 0xFF);
+    li[i] = lut((u >> 16) & 0xFF);
+  }
+}
+template <int MOD, class St>
+__device__ __forceinline__ void demap_pack_st(const uint32_t (&lr)[48], const uint32_t (&li)[48], St st) {
+  soft_units<MOD>(lr, li, st, std::make_integer_sequence<int, ModInfo<MOD>::ncbps / 16>{});
+}
 
 // ------------------------------------------------------------------ ChannelEqualization + PilotTrack
 // (receiver.blk:68-69).  Trig tables live in HBM, built once by the host

@@ -780,6 +780,9 @@ __global__ __launch_bounds__(1024) void k_pkt_rows(const int32_t* __restrict__ v
 // PERFLOG.md: symbol loads by LDS-DMA, with and without a one-iteration prefetch; the next
 // iteration's symbol prefetched into registers (233 VGPRs, 0.102 -> 0.110 ms); soft rows
 // stored by each lane.)
+#ifndef ZRX_DF_LUT_ONCE
+#define ZRX_DF_LUT_ONCE 1
+#endif
 #ifndef ZRX_DF_WAVES
 #define ZRX_DF_WAVES 4
 #endif
@@ -906,12 +909,25 @@ __global__ __launch_bounds__(kDfThreads) void k_data_fft(const uint4* __restrict
       uint4* row = stage + kDfRow * lane;
       auto st = [row](int q, uint4 v) { row[q] = v; };
       auto lu = [lut](uint32_t i) { return lut[i * kDfLutCopies]; };
+#if ZRX_DF_LUT_ONCE
+      // the LUT once for every lane, then the packing of the lane's modulation: a wave whose
+      // symbols mix modulations (config 5) no longer reads the LUT once per modulation present
+      uint32_t lr[48], li[48];
+      demap_lut_words(x, lu, lr, li);
+      switch (d.mod) {
+        case 0: demap_pack_st<0>(lr, li, st); break;
+        case 1: demap_pack_st<1>(lr, li, st); break;
+        case 2: demap_pack_st<2>(lr, li, st); break;
+        default: demap_pack_st<3>(lr, li, st); break;
+      }
+#else
       switch (d.mod) {
         case 0: demap_deinterleave_st<0>(x, lu, st); break;
         case 1: demap_deinterleave_st<1>(x, lu, st); break;
         case 2: demap_deinterleave_st<2>(x, lu, st); break;
         default: demap_deinterleave_st<3>(x, lu, st); break;
       }
+#endif
     }
     __builtin_amdgcn_wave_barrier();
     // ---- out: 18 x 64 units, (s, q) = divmod(64j + lane, 18)
