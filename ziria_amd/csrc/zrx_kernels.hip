@@ -930,19 +930,28 @@ __global__ __launch_bounds__(kDfThreads) void k_data_fft(const uint4* __restrict
 #endif
     }
     __builtin_amdgcn_wave_barrier();
-    // ---- out: 18 x 64 units, (s, q) = divmod(64j + lane, 18)
+    // ---- out: NU x 64 units, (s, q) = divmod(64j + lane, NU), NU = the wave's widest soft
+    // row (3, 6, 12 or 18 units): a wave of BPSK / QPSK / 16-QAM symbols (mixed batches) runs
+    // 3 / 6 / 12 store iterations, not 18
     // (lane0 is lane through an opaque move: the divmods are recomputed here each time
     // instead of being hoisted out of the loop as 54 live registers)
     int lane0;
     asm volatile("v_mov_b32 %0, %1" : "=v"(lane0) : "v"(lane));
+    auto out = [&](auto nc) {
+      constexpr int NU = decltype(nc)::value;
 #pragma unroll
-    for (int j = 0; j < 18; j++) {
-      const int u = 64 * j + lane0;
-      const int s = u / 18, q = u - 18 * s;
-      const uint32_t o = (uint32_t)__shfl((int)d.obase, s), nu = (uint32_t)__shfl((int)d.nu, s);
-      const uint4 v = stage[kDfRow * s + q];
-      if ((uint32_t)q < nu) soft[o + q] = v;
-    }
+      for (int j = 0; j < NU; j++) {
+        const int u = 64 * j + lane0;
+        const int s = u / NU, q = u - NU * s;
+        const uint32_t o = (uint32_t)__shfl((int)d.obase, s), nu = (uint32_t)__shfl((int)d.nu, s);
+        const uint4 v = stage[kDfRow * s + q];
+        if ((uint32_t)q < nu) soft[o + q] = v;
+      }
+    };
+    if (__builtin_amdgcn_ballot_w64(d.nu > 12u)) out(std::integral_constant<int, 18>{});
+    else if (__builtin_amdgcn_ballot_w64(d.nu > 6u)) out(std::integral_constant<int, 12>{});
+    else if (__builtin_amdgcn_ballot_w64(d.nu > 3u)) out(std::integral_constant<int, 6>{});
+    else out(std::integral_constant<int, 3>{});
     __builtin_amdgcn_wave_barrier();
     if (wn < nw) d = df_finish(n);
   }
