@@ -153,6 +153,23 @@ def test_chain_device_engine_54mbps(engine, oracle):
     assert all(r["crc_ok"] == 1 for r in ores)
 
 
+@pytest.mark.parametrize("mod,coding", [(0, 0), (0, 2), (1, 0), (1, 2), (2, 0), (2, 2), (3, 1), (3, 2)])
+def test_chain_uniform_mcs_vs_oracle(engine, oracle, mod, coding):
+    """Every 802.11a rate alone: waves of one modulation, so k_data_fft's store loop runs the
+    3 / 6 / 12 / 18 iterations of that soft row (the mixed tests run the widest of a wave)."""
+    b = txgen.make_batch(130, mod=mod, coding=coding, payload_len=211, sigma=2.0, seed=0x3C + 8 * mod + coding,
+                         device="cuda")
+    engine.reserve(130, b["max_nsym"])
+    pay, info = engine.rx(b["sym"], b["sym_off"], b["nsym"], b["max_nsym"])
+    pay, info = pay.cpu().numpy(), info.cpu().numpy()
+    assert (info[:, 0] == mod).all() and (info[:, 1] == coding).all() and (info[:, 4] == 1).all()
+    assert (pay[:, :211] == b["payload"]).all()
+    opay, ores = oracle.rx_batch_time(b["sym"].cpu().numpy(), b["sym_off"].cpu().numpy(),
+                                      b["nsym"].cpu().numpy(), nthreads=8)
+    assert all(r["crc_ok"] == 1 for r in ores)
+    assert (pay[:, :211] == opay[:, :211]).all()
+
+
 def test_chain_mixed_mcs_vs_oracle(engine, oracle):
     m = txgen.make_mixed(96, max_len=2200, sigma=3.0, seed=5, device="cuda")
     n = m["sym_off"].numel()
